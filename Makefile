@@ -1,0 +1,46 @@
+# Build of the MI355X bidirectional path tracer.
+#   libbdpt.so  : HIP kernels (gfx950) + C-ABI + host utilities   (the product)
+#   smallpt     : headless C host program, drop-in for smallpt_cpu.c's main/IdleFunc loop
+#   oracle/liboracle.so : CPU restatement used by tests/bench only (never linked by the product)
+# Everything builds with -ffp-contract=off: results must match the oracle bit for bit.
+
+PKG      := gpu_bidirectional_raytracer_amd
+CSRC     := $(PKG)/csrc
+BUILD    := $(PKG)/_build
+HIPCC    ?= /opt/rocm/bin/hipcc
+ARCH     ?= gfx950
+CC       ?= gcc
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function
+CFLAGS   := -O2 -std=gnu11 -fPIC -ffp-contract=off -Wall -Wextra -Wno-unused-parameter
+
+LIB      := $(PKG)/libbdpt.so
+HOST     := $(PKG)/smallpt
+ORACLE   := oracle/liboracle.so
+
+all: $(LIB) $(HOST) $(ORACLE)
+
+$(BUILD):
+	mkdir -p $(BUILD)
+
+$(BUILD)/bdpt_kernels.o: $(CSRC)/bdpt_kernels.hip $(CSRC)/bdpt_device.h | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(BUILD)/bdpt_host.o: $(CSRC)/bdpt_host.cpp $(CSRC)/bdpt_device.h include/bdpt.h | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(BUILD)/bdpt_util.o: $(CSRC)/bdpt_util.c include/bdpt.h | $(BUILD)
+	$(CC) $(CFLAGS) -c $< -o $@
+
+$(LIB): $(BUILD)/bdpt_kernels.o $(BUILD)/bdpt_host.o $(BUILD)/bdpt_util.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lm
+
+$(HOST): $(CSRC)/smallpt.c include/bdpt.h $(LIB)
+	$(CC) $(CFLAGS) -o $@ $< -L$(PKG) -lbdpt -lm -Wl,-rpath,'$$ORIGIN'
+
+$(ORACLE): oracle/bdpt_oracle.c include/bdpt.h
+	$(CC) -O2 -std=gnu11 -fPIC -shared -fopenmp -ffp-contract=off -Wall -o $@ $< -lm
+
+clean:
+	rm -rf $(BUILD) $(LIB) $(HOST) $(ORACLE)
+
+.PHONY: all clean

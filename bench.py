@@ -1,0 +1,220 @@
+#!/usr/bin/env python3
+"""bench.py -- path-pass throughput (Msamples/s) of the MI355X path tracer at 1080p cornell.scn.
+
+One "step" = `--passes` x N fused path passes (RadiancePathTracingKernel, device.cu:544) over this
+rank's pixel bands of the 1921x1081 frame (CLI 1920x1080 + the reference's +1).  Weak scaling:
+each rank owns 1/N of the pixels (16-row bands interleaved over ranks) and renders N x passes per
+step, so the per-GPU work is constant and the job renders N x the spp of the same frame.  The
+timed region ends with the RCCL (torch.distributed "nccl") sum-reduce of the radiance frame to
+rank 0, which assembles the image (pixels outside a rank's bands are zero, so the sum is exact).
+
+Prints ONE JSON line on rank 0 (see DESIGN.md "Measurement" for every field).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "Msamples/sec (rays·bounces/s) at 1080p cornell.scn, 1/2/4/8 GPU"
+
+# Per-sample work of the workload, measured once by the CPU restatement over the full 1921x1081
+# cornell frame (tests/test_work_model.py keeps these honest; DESIGN.md "Roofline").
+WORK = {
+    "cornell": {"sphere_tests": 129.47, "segments": 6.844, "diffuse": 6.139, "refr": 0.453,
+                "rng_reads": 27.007},
+}
+# FLOP model per primitive (DESIGN.md "Roofline"): sphere test 18, segment shading 28,
+# diffuse vertex (NEE to one light + VLP + new direction) 153, refraction 40, camera ray +
+# running mean 59.
+FLOP = {"sphere_tests": 18, "segments": 28, "diffuse": 153, "refr": 40, "per_sample": 59}
+ACCUM_BYTES_PER_PIXEL = 36       # colors 12R+12W, counter 4R+4W, pixels 4W per launch
+HBM_PEAK_GBS = 8000.0            # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP32_PEAK_TFLOPS = 157.3         # vector fp32 spec (FMA = 2 FLOP)
+FP32_NOFMA_TFLOPS = 78.6         # 256 CU x 128 lanes x 2.4 GHz, one mul/add per lane-cycle
+
+
+def flop_per_sample(w):
+    return (FLOP["sphere_tests"] * w["sphere_tests"] + FLOP["segments"] * w["segments"]
+            + FLOP["diffuse"] * w["diffuse"] + FLOP["refr"] * w["refr"] + FLOP["per_sample"])
+
+
+def cpu_baseline(sp, cam, W, H, sid, vlp, seconds):
+    """The oracle (CPU restatement) on this host's cores: a bounded sample of the same frame."""
+    import numpy as np
+    import oracle
+
+    threads = min(16, os.cpu_count() or 1)
+    rnd = oracle.mt607(0)
+    lp = oracle.light_pass(sp, rnd, 0)
+    t = time.perf_counter()
+    oracle.path_passes(sp, rnd, cam, W, H, lp, sid[:1], vlp[:1], nthreads=threads)
+    t_pass = time.perf_counter() - t
+    npass = max(1, min(len(sid), int(round(seconds / max(t_pass, 1e-3)))))
+    t = time.perf_counter()
+    oracle.path_passes(sp, rnd, cam, W, H, lp, sid[:npass], vlp[:npass], nthreads=threads)
+    dt = time.perf_counter() - t
+    # one core: every 4th 16-row band, one pass
+    t1, n1 = 0.0, 0
+    for y0 in range(0, H, 64):
+        y1 = min(H, y0 + 16)
+        t = time.perf_counter()
+        oracle.path_passes(sp, rnd, cam, W, H, lp, sid[:1], vlp[:1], rows=(y0, y1), nthreads=1)
+        t1 += time.perf_counter() - t
+        n1 += (y1 - y0) * W
+    return {"value": W * H * npass / dt / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/ CPU restatement, full {W}x{H} cornell frame x {npass} passes "
+                      f"(same sids as the GPU), OpenMP {threads} threads; 1-core: every 4th 16-row "
+                      f"band x 1 pass",
+            "value_1core": n1 / t1 / 1e6, "seconds": round(dt, 2)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--scene", default="cornell")
+    ap.add_argument("--width", type=int, default=1920, help="CLI width (internal = +1)")
+    ap.add_argument("--height", type=int, default=1080, help="CLI height (internal = +1)")
+    ap.add_argument("--passes", type=int, default=16, help="passes per step per GPU share")
+    ap.add_argument("--band-rows", type=int, default=16)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import numpy as np
+    import torch
+
+    import gpu_bidirectional_raytracer_amd as g
+
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    W, H = args.width + 1, args.height + 1                   # smallpt_cpu.c:409-410
+    cam, sp = g.read_scene(os.path.join(REPO, "assets", "scenes", args.scene + ".scn"))
+    g.update_camera(cam, W, H)
+    r = g.Renderer(sp, W, H, cam, device=local)
+    r.set_shard(rank, world, args.band_rows)
+    r.light_pass(0)                                           # UpdateRendering2
+    sched = g.PassScheduler()
+    sched.light()
+    per_step = args.passes * world
+    sid, vlp = sched.next(per_step * (args.warmup + args.steps))
+
+    def step(k):
+        a, b = k * per_step, (k + 1) * per_step
+        r.path_passes(sid[a:b], vlp[a:b], sync=False)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    for k in range(args.warmup):
+        step(k)
+    r.synchronize()
+    r.path_timing(reset=True)
+
+    # RCCL reduce target: torch tensors over the library's own device buffers (no copy)
+    col_ptr, cnt_ptr, _ = r.device_buffers()
+
+    class _Dev:
+        def __init__(self, ptr, n, typestr):
+            self.__cuda_array_interface__ = {"shape": (n,), "typestr": typestr,
+                                             "data": (ptr, False), "version": 3}
+
+    t_col = t_cnt = None
+    if dist is not None:
+        t_col = torch.as_tensor(_Dev(col_ptr, W * H * 3, "<f4"), device=f"cuda:{local}")
+        t_cnt = torch.as_tensor(_Dev(cnt_ptr, W * H, "<i4"), device=f"cuda:{local}")
+
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.warmup, args.warmup + args.steps):
+        step(k)
+    r.synchronize()
+    if dist is not None:                                      # assemble the frame on rank 0
+        dist.reduce(t_col, dst=0, op=dist.ReduceOp.SUM)
+        dist.reduce(t_cnt, dst=0, op=dist.ReduceOp.SUM)
+    torch.cuda.synchronize()
+    barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        tt = torch.tensor([dt], device=f"cuda:{local}", dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+
+    dev_ms, launches = r.path_timing()
+    samples = W * H * per_step * args.steps                   # every pixel exactly once per pass
+    value = samples / dt / 1e6
+
+    if rank == 0:
+        if dist is not None:
+            r.update_pixels()
+            cnt = t_cnt.cpu().numpy()
+            assert (cnt == per_step * (args.warmup + args.steps)).all(), "reduced counters wrong"
+        own_pixels = W * H // world if world == 1 else int(
+            sum(W * (min(H, y0 + args.band_rows) - y0) for y0 in range(0, H, args.band_rows)
+                if (y0 // args.band_rows) % world == rank))
+        w = WORK.get(args.scene)
+        avg_launch_s = dev_ms / 1e3 / max(launches, 1)
+        passes_per_launch = per_step * args.steps / max(launches, 1)
+        roofline = valu = None
+        if w is not None:
+            samples_per_launch = own_pixels * passes_per_launch
+            bytes_per_launch = own_pixels * ACCUM_BYTES_PER_PIXEL + samples_per_launch * 4 * w["rng_reads"]
+            achieved = bytes_per_launch / avg_launch_s / 1e9
+            traffic = None
+            pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
+            if os.path.exists(pmc):
+                rec = json.load(open(pmc))
+                if rec.get("scene") == args.scene and rec.get("passes_per_launch") == passes_per_launch \
+                        and rec.get("width") == W and rec.get("height") == H and world == 1:
+                    traffic = rec.get("hbm_bytes_per_launch")
+            roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                        "bytes_per_launch": int(bytes_per_launch), "avg_launch_ms": round(avg_launch_s * 1e3, 4),
+                        "launches": launches}
+            fl = flop_per_sample(w) * samples_per_launch / avg_launch_s / 1e12
+            valu = {"achieved": round(fl, 2), "unit": "TFLOP/s", "peak": FP32_PEAK_TFLOPS,
+                    "frac": round(fl / FP32_PEAK_TFLOPS, 4), "peak_no_fma": FP32_NOFMA_TFLOPS,
+                    "frac_no_fma": round(fl / FP32_NOFMA_TFLOPS, 4),
+                    "flop_per_sample": round(flop_per_sample(w), 1),
+                    "note": "bound: fp32 VALU (no contraction, correctly rounded div/sqrt); "
+                            "FLOP model in DESIGN.md"}
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(sp, cam, W, H, sid, vlp, args.cpu_seconds)
+        line = {
+            "metric": METRIC, "value": round(value, 2), "unit": "Msamples/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "data": "synthetic: reference cornell.scn + MT607 table (seed 0) + glibc-rand pass offsets",
+            "config": {"workload": f"{args.scene}.scn {W}x{H} internal (CLI {args.width}x{args.height}), "
+                                   f"<=7-segment eye paths + NEE + 1 VLP per diffuse vertex",
+                       "scene": args.scene, "width": W, "height": H, "passes_per_step": per_step,
+                       "spp_total": per_step * (args.warmup + args.steps),
+                       "parallelism": f"pixel bands x{world} ({args.band_rows}-row, interleaved)"},
+            "device_ms_per_step": round(dev_ms / args.steps, 3),
+            "roofline": roofline, "valu": valu, "cpu_baseline": cpu,
+        }
+        if cpu:
+            line["speedup_vs_cpu"] = round(value / cpu["value"], 1)
+        print(json.dumps(line), flush=True)
+    r.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

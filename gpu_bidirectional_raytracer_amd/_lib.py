@@ -1,0 +1,121 @@
+"""ctypes binding of the C-ABI in include/bdpt.h (libbdpt.so, built in-tree by `make`).
+
+The product path has no fallback: if the HIP library is missing this module raises on import.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libbdpt.so")
+REPO_ROOT = os.path.dirname(_HERE)
+DEFAULT_DAT = os.path.join(REPO_ROOT, "assets", "data", "MersenneTwister.dat")
+SCENE_DIR = os.path.join(REPO_ROOT, "assets", "scenes")
+
+RAND_N = 4096 * 1876
+LIGHT_POINTS = 4096
+COUNTER_CAP = 30000
+
+BDPT_OK, BDPT_EINVAL, BDPT_EIO, BDPT_EHIP, BDPT_ENOMEM, BDPT_ESTATE = 0, -1, -2, -3, -4, -5
+DIFF, SPEC, REFR, LITE = 0, 1, 2, 3
+KEY_UP, KEY_DOWN, KEY_LEFT, KEY_RIGHT, KEY_PAGE_UP, KEY_PAGE_DOWN = range(0x101, 0x107)
+
+
+class Vec(ctypes.Structure):
+    _fields_ = [("x", ctypes.c_float), ("y", ctypes.c_float), ("z", ctypes.c_float)]
+
+    def __iter__(self):
+        return iter((self.x, self.y, self.z))
+
+    def __repr__(self):
+        return f"Vec({self.x!r}, {self.y!r}, {self.z!r})"
+
+
+class Sphere(ctypes.Structure):
+    _fields_ = [("rad", ctypes.c_float), ("p", Vec), ("e", Vec), ("c", Vec), ("refl", ctypes.c_int)]
+
+
+class LightPath(ctypes.Structure):
+    _fields_ = [("hp", Vec), ("rad", Vec), ("nl", Vec)]
+
+
+class Camera(ctypes.Structure):
+    _fields_ = [("orig", Vec), ("target", Vec), ("dir", Vec), ("x", Vec), ("y", Vec)]
+
+
+class RandState(ctypes.Structure):
+    _fields_ = [("state", ctypes.c_int * 31), ("f", ctypes.c_int), ("r", ctypes.c_int)]
+
+
+class PassState(ctypes.Structure):
+    _fields_ = [("rng", RandState), ("flag", ctypes.c_int), ("vlp_index", ctypes.c_int)]
+
+
+assert ctypes.sizeof(Vec) == 12 and ctypes.sizeof(Sphere) == 44
+assert ctypes.sizeof(LightPath) == 36 and ctypes.sizeof(Camera) == 60
+
+# every symbol include/bdpt.h declares: (name, restype, argtypes)
+_P = ctypes.c_void_p
+_SIGS = [
+    ("bdpt_create", ctypes.c_int, [ctypes.POINTER(_P), ctypes.POINTER(Sphere), ctypes.c_uint,
+                                    ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]),
+    ("bdpt_destroy", None, [_P]),
+    ("bdpt_last_error", ctypes.c_char_p, [_P]),
+    ("bdpt_create_error", ctypes.c_char_p, []),
+    ("bdpt_set_scene", ctypes.c_int, [_P, ctypes.POINTER(Sphere), ctypes.c_uint]),
+    ("bdpt_set_camera", ctypes.c_int, [_P, ctypes.POINTER(Camera)]),
+    ("bdpt_reset_accum", ctypes.c_int, [_P]),
+    ("bdpt_set_shard", ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    ("bdpt_light_pass", ctypes.c_int, [_P, ctypes.c_int]),
+    ("bdpt_generate_rand", ctypes.c_int, [_P, ctypes.c_uint]),
+    ("bdpt_path_passes", ctypes.c_int, [_P, _P, _P, ctypes.c_int]),
+    ("bdpt_synchronize", ctypes.c_int, [_P]),
+    ("bdpt_last_path_ms", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_float)]),
+    ("bdpt_path_timing", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double),
+                                         ctypes.POINTER(ctypes.c_longlong), ctypes.c_int]),
+    ("bdpt_read_radiance", ctypes.c_int, [_P, _P, _P]),
+    ("bdpt_read_pixels", ctypes.c_int, [_P, _P]),
+    ("bdpt_read_rand", ctypes.c_int, [_P, _P]),
+    ("bdpt_read_lightpaths", ctypes.c_int, [_P, _P]),
+    ("bdpt_device_buffers", ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.POINTER(_P), ctypes.POINTER(_P)]),
+    ("bdpt_update_pixels", ctypes.c_int, [_P]),
+    ("bdpt_read_scene", ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(Camera),
+                                        ctypes.POINTER(ctypes.POINTER(Sphere)), ctypes.POINTER(ctypes.c_uint)]),
+    ("bdpt_free_scene", None, [ctypes.POINTER(Sphere)]),
+    ("bdpt_default_scene", ctypes.c_uint, [ctypes.POINTER(Camera), ctypes.POINTER(Sphere)]),
+    ("bdpt_update_camera", None, [ctypes.POINTER(Camera), ctypes.c_int, ctypes.c_int]),
+    ("bdpt_camera_key", ctypes.c_int, [ctypes.POINTER(Camera), ctypes.c_int]),
+    ("bdpt_sphere_key", ctypes.c_int, [ctypes.POINTER(Sphere), ctypes.c_uint, ctypes.c_int, ctypes.c_int]),
+    ("bdpt_save_ppm", ctypes.c_int, [ctypes.c_char_p, _P, ctypes.c_int, ctypes.c_int]),
+    ("bdpt_gamma_thresholds", None, [_P]),
+    ("bdpt_srand", None, [ctypes.POINTER(RandState), ctypes.c_uint]),
+    ("bdpt_rand", ctypes.c_int, [ctypes.POINTER(RandState)]),
+    ("bdpt_pass_state_init", None, [ctypes.POINTER(PassState)]),
+    ("bdpt_pass_state_light", None, [ctypes.POINTER(PassState)]),
+    ("bdpt_pass_state_next", None, [ctypes.POINTER(PassState), ctypes.POINTER(ctypes.c_uint),
+                                     ctypes.POINTER(ctypes.c_int)]),
+    ("bdpt_pass_schedule", None, [ctypes.POINTER(PassState), ctypes.c_int, _P, _P]),
+]
+EXPORTED = [s[0] for s in _SIGS]
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is not built: run `make` (or __graft_entry__.build()) first; "
+                          "there is no CPU fallback for the render path")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, res, args in _SIGS:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+class BdptError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"bdpt error {code}: {msg}")
+        self.code = code

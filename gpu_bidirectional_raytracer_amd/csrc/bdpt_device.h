@@ -1,0 +1,74 @@
+// bdpt_device.h -- device-side data layout shared by the HIP kernels and the host launcher.
+//
+// HBM layout (one context = one GPU):
+//   d_rand    float[7,684,096]      MT607 table, lane-major (tid + k*4096)      30.7 MB
+//   d_lp      bdpt_dev_lightpath[4096]  VLPs {hp, rad, nl}, AoS 36 B            147 KB
+//   d_sph     bdpt_dev_sphere[n]    48 B/sphere {p, rad^2, e, rad, c, refl}
+//   d_colors  bdpt_dev_vec[W*H]     running-mean radiance, AoS 12 B (== dev_colors)
+//   d_counter unsigned[W*H]         samples per pixel (== dev_counter)
+//   d_pixels  uchar4[W*H]           gamma-2.2 8-bit RGBA (== pixels_buf)
+#ifndef BDPT_DEVICE_H
+#define BDPT_DEVICE_H
+
+#include <hip/hip_runtime.h>
+
+#define BDPT_DEV_RAND_N (4096u * 1876u)
+#define BDPT_DEV_N_PER_RNG 1876
+#define BDPT_DEV_LIGHT_POINTS 4096
+#define BDPT_DEV_COUNTER_CAP 30000u
+#define BDPT_DEV_DIFF 0
+#define BDPT_DEV_SPEC 1
+#define BDPT_DEV_REFR 2
+
+struct bdpt_dev_vec { float x, y, z; };
+struct bdpt_dev_lightpath { float hx, hy, hz, rx, ry, rz, nx, ny, nz; };
+struct bdpt_dev_sphere {
+    float px, py, pz, rr;     // rr = rad*rad (the float product SphereIntersectDevice forms)
+    float ex, ey, ez, rad;
+    float cx, cy, cz;
+    int refl;
+};
+
+struct bdpt_path_args {
+    const bdpt_dev_sphere* sph;
+    unsigned n;
+    unsigned n_lights;
+    const int* lights;              // indices of emitters (e != 0), ascending
+    const float* rnd;
+    const bdpt_dev_lightpath* lp;
+    const unsigned* sid;            // per pass
+    const int* vlp;                 // per pass
+    int npass;
+    bdpt_dev_vec* colors;
+    unsigned* counter;
+    uchar4* pixels;
+    const float* gamma_thr;         // 256 thresholds of toInt (vec.h:34)
+    int W, H;
+    float inv_w, inv_h;             // (float)(14./W), (float)(10.5/H)
+    double half_w, half_h;          // (double)(inv_w*W)/2., (double)(inv_h*H)/2.
+    float ux[3], uy[3], ud[3], orig[3];
+    float tx, ty, tz;
+    int shard, nshards, band_rows;
+};
+
+// toInt (vec.h:34) by threshold search: thr[k] is the smallest float whose toInt is >= k,
+// computed on the host with the same pow as the reference semantics; 8 compares per channel.
+__device__ __forceinline__ int bdpt_dev_gamma8(float v, const float* __restrict__ thr) {
+    int k = 0;
+#pragma unroll
+    for (int step = 128; step > 0; step >>= 1)
+        if (v >= thr[k + step]) k += step;
+    return k;
+}
+
+__device__ __forceinline__ uchar4 bdpt_dev_to_rgba(float r, float g, float b,
+                                                   const float* __restrict__ thr) {
+    uchar4 o;
+    o.x = (unsigned char)bdpt_dev_gamma8(r, thr);
+    o.y = (unsigned char)bdpt_dev_gamma8(g, thr);
+    o.z = (unsigned char)bdpt_dev_gamma8(b, thr);
+    o.w = 0;
+    return o;
+}
+
+#endif

@@ -1,0 +1,427 @@
+// bdpt_host.cpp -- the C-ABI (include/bdpt.h) over the HIP kernels of bdpt_kernels.hip.
+//
+// Replaces the device-buffer globals and kernel launches of src/smallpt_cpu.c
+// (AllocateBuffers :153, FreeBuffers :98, UpdateRendering :265, UpdateRendering2 :300) and
+// loadMTGPU/seedMTGPU of src/MersenneTwister_kernel.cu:23-51.  One context = one GPU + one
+// HIP stream.  Every HIP call is checked; failures return BDPT_EHIP with the HIP message in
+// bdpt_last_error() (the reference prints and continues; the host shell decides).
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <vector>
+
+#include "../../include/bdpt.h"
+#include "bdpt_device.h"
+
+static_assert(sizeof(bdpt_vec) == 12, "Vec is 12 B (vec.h:4-6)");
+static_assert(sizeof(bdpt_ray) == 24, "Ray is 24 B (geom.h:9-11)");
+static_assert(sizeof(bdpt_sphere) == 44, "Sphere is 44 B (geom.h:23-27)");
+static_assert(sizeof(bdpt_lightpath) == 36, "LightPath is 36 B (geom.h:29-33)");
+static_assert(sizeof(bdpt_camera) == 60, "Camera is 60 B (camera.h:7-12)");
+static_assert(sizeof(bdpt_dev_lightpath) == sizeof(bdpt_lightpath), "VLP layout");
+static_assert(sizeof(bdpt_dev_vec) == sizeof(bdpt_vec), "colour layout");
+
+extern "C" __global__ void bdpt_mt607_kernel(const uint4*, unsigned, float*);
+extern "C" __global__ void bdpt_light_kernel(const bdpt_dev_sphere*, unsigned, const float*, int,
+                                             bdpt_dev_lightpath*);
+extern "C" __global__ void bdpt_path_kernel(bdpt_path_args);
+extern "C" __global__ void bdpt_pixels_kernel(const bdpt_dev_vec*, uchar4*, const float*, int);
+
+// gamma thresholds (host, once): see bdpt_util.c
+extern "C" void bdpt_gamma_thresholds(float thr[256]);
+
+struct bdpt_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool timed = false;          // an event pair of a path-pass call is outstanding
+    int timed_launches = 0;      // kernel launches inside that pair
+    double acc_ms = 0.0;         // accumulated device time of finished path-pass calls
+    long long acc_launches = 0;
+    float last_ms = 0.f;
+    int W = 0, H = 0;
+    std::vector<bdpt_sphere> spheres;
+    std::vector<int> lights;
+    bdpt_camera cam{};
+    bool cam_set = false;
+    bool rand_ready = false;
+    int shard = 0, nshards = 1, band_rows = 16;
+    uint4* d_params = nullptr;          // 4096 x {matrix_a, mask_b, mask_c, seed}
+    float* d_rand = nullptr;
+    bdpt_dev_lightpath* d_lp = nullptr;
+    bdpt_dev_sphere* d_sph = nullptr;
+    unsigned sph_cap = 0;
+    int* d_lights = nullptr;
+    bdpt_dev_vec* d_colors = nullptr;
+    unsigned* d_counter = nullptr;
+    uchar4* d_pixels = nullptr;
+    float* d_thr = nullptr;
+    unsigned* d_sid = nullptr;
+    int* d_vlp = nullptr;
+    int pass_cap = 0;
+    uint32_t h_params[4 * BDPT_MT_RNG_COUNT];
+    char err[512] = {0};
+};
+
+static int fail(bdpt_ctx* c, int code, const char* fmt, ...) {
+    if (c) {
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(c->err, sizeof(c->err), fmt, ap);
+        va_end(ap);
+    }
+    return code;
+}
+
+#define HIPCHK(ctx, call)                                                                      \
+    do {                                                                                       \
+        hipError_t e_ = (call);                                                                \
+        if (e_ != hipSuccess)                                                                  \
+            return fail((ctx), BDPT_EHIP, "%s: %s", #call, hipGetErrorString(e_));            \
+    } while (0)
+
+static int upload_scene(bdpt_ctx* c) {
+    const unsigned n = (unsigned)c->spheres.size();
+    std::vector<bdpt_dev_sphere> ds(n);
+    c->lights.clear();
+    for (unsigned i = 0; i < n; i++) {
+        const bdpt_sphere& s = c->spheres[i];
+        bdpt_dev_sphere& d = ds[i];
+        d.px = s.p.x; d.py = s.p.y; d.pz = s.p.z;
+        d.rr = s.rad * s.rad;                       // the product SphereIntersectDevice forms
+        d.ex = s.e.x; d.ey = s.e.y; d.ez = s.e.z;
+        d.rad = s.rad;
+        d.cx = s.c.x; d.cy = s.c.y; d.cz = s.c.z;
+        d.refl = s.refl;
+        if (!(s.e.x == 0.f && s.e.y == 0.f && s.e.z == 0.f)) c->lights.push_back((int)i);
+    }
+    if (n > c->sph_cap) {
+        if (c->d_sph) HIPCHK(c, hipFree(c->d_sph));
+        if (c->d_lights) HIPCHK(c, hipFree(c->d_lights));
+        c->d_sph = nullptr; c->d_lights = nullptr;
+        HIPCHK(c, hipMalloc(&c->d_sph, sizeof(bdpt_dev_sphere) * n));
+        HIPCHK(c, hipMalloc(&c->d_lights, sizeof(int) * n));
+        c->sph_cap = n;
+    }
+    HIPCHK(c, hipMemcpyAsync(c->d_sph, ds.data(), sizeof(bdpt_dev_sphere) * n, hipMemcpyHostToDevice, c->stream));
+    if (!c->lights.empty())
+        HIPCHK(c, hipMemcpyAsync(c->d_lights, c->lights.data(), sizeof(int) * c->lights.size(),
+                                 hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return BDPT_OK;
+}
+
+static void release(bdpt_ctx* c) {
+    void* bufs[] = {c->d_params, c->d_rand, c->d_lp, c->d_sph, c->d_lights, c->d_colors,
+                    c->d_counter, c->d_pixels, c->d_thr, c->d_sid, c->d_vlp};
+    for (void* b : bufs)
+        if (b) (void)hipFree(b);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+}
+
+// Fold the outstanding event pair (if any) into the accumulators.  Caller has synchronised.
+static int fold_timing(bdpt_ctx* c) {
+    if (!c->timed) return BDPT_OK;
+    float ms = 0.f;
+    HIPCHK(c, hipEventSynchronize(c->ev1));
+    HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    c->last_ms = ms;
+    c->acc_ms += ms;
+    c->acc_launches += c->timed_launches;
+    c->timed = false;
+    return BDPT_OK;
+}
+
+extern "C" {
+
+const char* bdpt_last_error(const bdpt_ctx* c) { return c ? c->err : "null context"; }
+
+static char g_create_err[512];
+
+int bdpt_create(bdpt_ctx** out, const bdpt_sphere* spheres, unsigned n, int W, int H,
+                const char* mt_dat_path, int device) {
+    if (!out) return BDPT_EINVAL;
+    *out = nullptr;
+    bdpt_ctx* c = new (std::nothrow) bdpt_ctx();
+    if (!c) return BDPT_ENOMEM;
+    int rc = BDPT_OK;
+    auto bail = [&](int code) {
+        snprintf(g_create_err, sizeof(g_create_err), "%s", c->err);
+        release(c);
+        delete c;
+        return code;
+    };
+    if (W <= 0 || H <= 0 || (long)W * (long)H > (1L << 30) || (n > 0 && !spheres))
+        return (fail(c, BDPT_EINVAL, "bdpt_create: bad size %dx%d or spheres", W, H), bail(BDPT_EINVAL));
+    c->W = W; c->H = H; c->device = device;
+    c->spheres.assign(spheres, spheres + n);
+    // loadMTGPU (MersenneTwister_kernel.cu:23-36): 4096 x 16 B records
+    FILE* f = fopen(mt_dat_path ? mt_dat_path : "assets/data/MersenneTwister.dat", "rb");
+    if (!f) return (fail(c, BDPT_EIO, "initMTGPU(): failed to open %s", mt_dat_path), bail(BDPT_EIO));
+    size_t got = fread(c->h_params, sizeof(c->h_params), 1, f);
+    fclose(f);
+    if (got != 1) return (fail(c, BDPT_EIO, "initMTGPU(): failed to load %s", mt_dat_path), bail(BDPT_EIO));
+
+#define CK(call) do { hipError_t e_ = (call); if (e_ != hipSuccess) { \
+        fail(c, BDPT_EHIP, "%s: %s", #call, hipGetErrorString(e_)); return bail(BDPT_EHIP); } } while (0)
+    CK(hipSetDevice(device));
+    CK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    CK(hipEventCreate(&c->ev0));
+    CK(hipEventCreate(&c->ev1));
+    const size_t np = (size_t)W * H;
+    CK(hipMalloc(&c->d_params, sizeof(c->h_params)));
+    CK(hipMalloc(&c->d_rand, sizeof(float) * BDPT_RAND_N));
+    CK(hipMalloc(&c->d_lp, sizeof(bdpt_dev_lightpath) * BDPT_LIGHT_POINTS));
+    CK(hipMalloc(&c->d_colors, sizeof(bdpt_dev_vec) * np));
+    CK(hipMalloc(&c->d_counter, sizeof(unsigned) * np));
+    CK(hipMalloc(&c->d_pixels, sizeof(uchar4) * np));
+    CK(hipMalloc(&c->d_thr, sizeof(float) * 256));
+    CK(hipMemsetAsync(c->d_lp, 0, sizeof(bdpt_dev_lightpath) * BDPT_LIGHT_POINTS, c->stream));
+    CK(hipMemsetAsync(c->d_colors, 0, sizeof(bdpt_dev_vec) * np, c->stream));
+    CK(hipMemsetAsync(c->d_counter, 0, sizeof(unsigned) * np, c->stream));
+    CK(hipMemsetAsync(c->d_pixels, 0, sizeof(uchar4) * np, c->stream));
+    float thr[256];
+    bdpt_gamma_thresholds(thr);
+    CK(hipMemcpyAsync(c->d_thr, thr, sizeof(thr), hipMemcpyHostToDevice, c->stream));
+    CK(hipStreamSynchronize(c->stream));
+#undef CK
+    rc = upload_scene(c);
+    if (rc != BDPT_OK) return bail(rc);
+    *out = c;
+    return BDPT_OK;
+}
+
+const char* bdpt_create_error(void) { return g_create_err; }
+
+void bdpt_destroy(bdpt_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    release(c);
+    delete c;
+}
+
+int bdpt_set_scene(bdpt_ctx* c, const bdpt_sphere* spheres, unsigned n) {
+    if (!c || (n > 0 && !spheres)) return BDPT_EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    c->spheres.assign(spheres, spheres + n);
+    return upload_scene(c);
+}
+
+int bdpt_set_camera(bdpt_ctx* c, const bdpt_camera* cam) {
+    if (!c || !cam) return BDPT_EINVAL;
+    c->cam = *cam;
+    c->cam_set = true;
+    return BDPT_OK;
+}
+
+int bdpt_reset_accum(bdpt_ctx* c) {
+    if (!c) return BDPT_EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemsetAsync(c->d_counter, 0, sizeof(unsigned) * (size_t)c->W * c->H, c->stream));
+    return BDPT_OK;
+}
+
+int bdpt_set_shard(bdpt_ctx* c, int shard, int nshards, int band_rows) {
+    if (!c || nshards < 1 || shard < 0 || shard >= nshards || band_rows < 1)
+        return c ? fail(c, BDPT_EINVAL, "bdpt_set_shard: bad shard %d/%d band %d", shard, nshards, band_rows)
+                 : BDPT_EINVAL;
+    c->shard = shard; c->nshards = nshards; c->band_rows = band_rows;
+    return BDPT_OK;
+}
+
+int bdpt_generate_rand(bdpt_ctx* c, unsigned seed) {
+    if (!c) return BDPT_EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    // seedMTGPU(seed): every record's seed field := seed (MersenneTwister_kernel.cu:44-47)
+    std::vector<uint32_t> p(c->h_params, c->h_params + 4 * BDPT_MT_RNG_COUNT);
+    for (int i = 0; i < BDPT_MT_RNG_COUNT; i++) p[4 * i + 3] = seed;
+    HIPCHK(c, hipMemcpyAsync(c->d_params, p.data(), sizeof(uint32_t) * p.size(), hipMemcpyHostToDevice, c->stream));
+    hipLaunchKernelGGL(bdpt_mt607_kernel, dim3(BDPT_MT_RNG_COUNT / 64), dim3(64), 0, c->stream,
+                       (const uint4*)c->d_params, seed, c->d_rand);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->rand_ready = true;
+    return BDPT_OK;
+}
+
+int bdpt_light_pass(bdpt_ctx* c, int current_sample) {
+    if (!c) return BDPT_EINVAL;
+    if (c->lights.empty()) return BDPT_OK;                 // the reference launches nothing
+    // The reference regenerates the table per light with the same seed (smallpt_cpu.c:321-322):
+    // one generation is identical.
+    int rc = bdpt_generate_rand(c, (unsigned)(current_sample * 5));
+    if (rc) return rc;
+    hipLaunchKernelGGL(bdpt_light_kernel, dim3(BDPT_LIGHT_POINTS / 64), dim3(64), 0, c->stream,
+                       (const bdpt_dev_sphere*)c->d_sph, (unsigned)c->spheres.size(),
+                       (const float*)c->d_rand, current_sample, c->d_lp);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return BDPT_OK;
+}
+
+// camera terms of device.cu:572-592, with the kernel's float operation order
+static void vnorm3(float v[3]) {
+    float l = 1.f / sqrtf(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+    v[0] = l * v[0]; v[1] = l * v[1]; v[2] = l * v[2];
+}
+
+int bdpt_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int npass) {
+    if (!c) return BDPT_EINVAL;
+    if (npass < 0 || (npass > 0 && (!sid || !vlp))) return fail(c, BDPT_EINVAL, "bdpt_path_passes: bad pass list");
+    if (npass == 0) return BDPT_OK;
+    if (!c->rand_ready) return fail(c, BDPT_ESTATE, "bdpt_path_passes: no random table (run the light pass first)");
+    if (!c->cam_set) return fail(c, BDPT_ESTATE, "bdpt_path_passes: camera not set");
+    HIPCHK(c, hipSetDevice(c->device));
+    // the previous launch may still read d_sid/d_vlp: drain the stream before overwriting them
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (int rc = fold_timing(c)) return rc;
+    if (npass > c->pass_cap) {
+        if (c->d_sid) HIPCHK(c, hipFree(c->d_sid));
+        if (c->d_vlp) HIPCHK(c, hipFree(c->d_vlp));
+        c->d_sid = nullptr; c->d_vlp = nullptr;
+        int cap = npass < 1024 ? 1024 : npass;
+        HIPCHK(c, hipMalloc(&c->d_sid, sizeof(unsigned) * cap));
+        HIPCHK(c, hipMalloc(&c->d_vlp, sizeof(int) * cap));
+        c->pass_cap = cap;
+    }
+    HIPCHK(c, hipMemcpy(c->d_sid, sid, sizeof(unsigned) * npass, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->d_vlp, vlp, sizeof(int) * npass, hipMemcpyHostToDevice));
+
+    bdpt_path_args a;
+    memset(&a, 0, sizeof(a));
+    a.sph = c->d_sph;
+    a.n = (unsigned)c->spheres.size();
+    a.n_lights = (unsigned)c->lights.size();
+    a.lights = c->d_lights;
+    a.rnd = c->d_rand;
+    a.lp = c->d_lp;
+    a.colors = c->d_colors;
+    a.counter = c->d_counter;
+    a.pixels = c->d_pixels;
+    a.gamma_thr = c->d_thr;
+    a.W = c->W; a.H = c->H;
+    a.inv_w = (float)(14. / c->W);                       // smallpt_cpu.c:411-412
+    a.inv_h = (float)(10.5 / c->H);
+    a.half_w = (double)(a.inv_w * (float)c->W) / 2.;      // device.cu:565 inv_width*width/2.
+    a.half_h = (double)(a.inv_h * (float)c->H) / 2.;
+    const bdpt_camera& cam = c->cam;
+    float ux[3] = {cam.x.x, cam.x.y, cam.x.z}, uy[3] = {cam.y.x, cam.y.y, cam.y.z};
+    float ud[3] = {cam.dir.x, cam.dir.y, cam.dir.z};
+    vnorm3(ux); vnorm3(uy); vnorm3(ud);
+    float nx[3] = {-1.f * cam.x.x, -1.f * cam.x.y, -1.f * cam.x.z};
+    float ny[3] = {-1.f * cam.y.x, -1.f * cam.y.y, -1.f * cam.y.z};
+    float nd[3] = {-1.f * cam.dir.x, -1.f * cam.dir.y, -1.f * cam.dir.z};
+    vnorm3(nx); vnorm3(ny);                               // :584-590 (no vnorm on -dir, :591)
+    a.tx = nx[0] * cam.orig.x + nx[1] * cam.orig.y + nx[2] * cam.orig.z;
+    a.ty = ny[0] * cam.orig.x + ny[1] * cam.orig.y + ny[2] * cam.orig.z;
+    a.tz = nd[0] * cam.orig.x + nd[1] * cam.orig.y + nd[2] * cam.orig.z;
+    memcpy(a.ux, ux, sizeof(ux)); memcpy(a.uy, uy, sizeof(uy)); memcpy(a.ud, ud, sizeof(ud));
+    a.orig[0] = cam.orig.x; a.orig[1] = cam.orig.y; a.orig[2] = cam.orig.z;
+    a.shard = c->shard; a.nshards = c->nshards; a.band_rows = c->band_rows;
+
+    dim3 grid((c->W + 15) / 16, (c->H + 15) / 16), block(256);
+    const size_t smem = sizeof(float4) * 4 * (a.n ? a.n : 1);
+    // keep single launches bounded (~2^28 samples) so no dispatch runs for many seconds
+    const long per_pass = (long)c->W * c->H;
+    int chunk = (int)((1L << 28) / (per_pass > 0 ? per_pass : 1));
+    if (chunk < 1) chunk = 1;
+    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+    int launches = 0;
+    for (int p0 = 0; p0 < npass; p0 += chunk, launches++) {
+        a.sid = c->d_sid + p0;
+        a.vlp = c->d_vlp + p0;
+        a.npass = npass - p0 < chunk ? npass - p0 : chunk;
+        hipLaunchKernelGGL(bdpt_path_kernel, grid, block, smem, c->stream, a);
+        HIPCHK(c, hipGetLastError());
+    }
+    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+    c->timed = true;
+    c->timed_launches = launches;
+    return BDPT_OK;
+}
+
+int bdpt_synchronize(bdpt_ctx* c) {
+    if (!c) return BDPT_EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return fold_timing(c);
+}
+
+int bdpt_last_path_ms(bdpt_ctx* c, float* ms) {
+    if (!c || !ms) return BDPT_EINVAL;
+    if (int rc = bdpt_synchronize(c)) return rc;
+    if (c->acc_launches == 0) return fail(c, BDPT_ESTATE, "bdpt_last_path_ms: no path pass launched");
+    *ms = c->last_ms;
+    return BDPT_OK;
+}
+
+int bdpt_path_timing(bdpt_ctx* c, double* total_ms, long long* launches, int reset) {
+    if (!c) return BDPT_EINVAL;
+    if (int rc = bdpt_synchronize(c)) return rc;
+    if (total_ms) *total_ms = c->acc_ms;
+    if (launches) *launches = c->acc_launches;
+    if (reset) { c->acc_ms = 0.0; c->acc_launches = 0; }
+    return BDPT_OK;
+}
+
+int bdpt_read_radiance(bdpt_ctx* c, bdpt_vec* colors, unsigned* counter) {
+    if (!c) return BDPT_EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    const size_t np = (size_t)c->W * c->H;
+    if (colors) HIPCHK(c, hipMemcpyAsync(colors, c->d_colors, sizeof(bdpt_vec) * np, hipMemcpyDeviceToHost, c->stream));
+    if (counter) HIPCHK(c, hipMemcpyAsync(counter, c->d_counter, sizeof(unsigned) * np, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return BDPT_OK;
+}
+
+int bdpt_read_pixels(bdpt_ctx* c, unsigned char* rgba) {
+    if (!c || !rgba) return BDPT_EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemcpyAsync(rgba, c->d_pixels, 4 * (size_t)c->W * c->H, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return BDPT_OK;
+}
+
+int bdpt_read_rand(bdpt_ctx* c, float* t) {
+    if (!c || !t) return BDPT_EINVAL;
+    if (!c->rand_ready) return fail(c, BDPT_ESTATE, "bdpt_read_rand: table not generated");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemcpyAsync(t, c->d_rand, sizeof(float) * BDPT_RAND_N, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return BDPT_OK;
+}
+
+int bdpt_read_lightpaths(bdpt_ctx* c, bdpt_lightpath* lp) {
+    if (!c || !lp) return BDPT_EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemcpyAsync(lp, c->d_lp, sizeof(bdpt_lightpath) * BDPT_LIGHT_POINTS, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return BDPT_OK;
+}
+
+int bdpt_device_buffers(bdpt_ctx* c, void** colors, void** counter, void** pixels) {
+    if (!c) return BDPT_EINVAL;
+    if (colors) *colors = c->d_colors;
+    if (counter) *counter = c->d_counter;
+    if (pixels) *pixels = c->d_pixels;
+    return BDPT_OK;
+}
+
+int bdpt_update_pixels(bdpt_ctx* c) {
+    if (!c) return BDPT_EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    const int np = c->W * c->H;
+    hipLaunchKernelGGL(bdpt_pixels_kernel, dim3((np + 255) / 256), dim3(256), 0, c->stream,
+                       (const bdpt_dev_vec*)c->d_colors, c->d_pixels, (const float*)c->d_thr, np);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return BDPT_OK;
+}
+
+}  // extern "C"

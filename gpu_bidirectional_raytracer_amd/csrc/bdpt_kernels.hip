@@ -1,0 +1,429 @@
+// bdpt_kernels.hip -- hand-written HIP kernels for gfx950 (MI355X, CDNA4) implementing the render
+// path of sim186/gpu_bidirectional_raytracer: the MT607 random table, the light pass (VLP
+// creation) and the per-pixel eye-path integrator with NEE + VLP connection.
+//
+// Numerics contract (shared with the CPU oracle): fp32 with NO contraction
+// (built with -ffp-contract=off), correctly rounded fp32 div/sqrt (hipcc default), the fp64 camera
+// steps of device.cu:565-566,594 kept in fp64, and sinf/cosf evaluated as (float)sincos((double)x).
+// Every float operation below is in the reference's order; reordering any of them changes
+// results (SURVEY.md 7 "Hard parts").
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <utility>
+#include "bdpt_device.h"
+
+namespace {
+
+// ---------------------------------------------------------------------------------------------
+// small float3 helpers with the reference's operation order (vec.h:12-25)
+struct f3 { float x, y, z; };
+__device__ __forceinline__ f3 mk(float a, float b, float c) { f3 v; v.x = a; v.y = b; v.z = c; return v; }
+__device__ __forceinline__ f3 add(f3 a, f3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ f3 sub(f3 a, f3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ f3 mul(f3 a, f3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
+__device__ __forceinline__ f3 smul(float k, f3 b) { return mk(k * b.x, k * b.y, k * b.z); }
+__device__ __forceinline__ float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ f3 norm(f3 v) { float l = 1.f / sqrtf(dot(v, v)); return smul(l, v); }
+__device__ __forceinline__ f3 cross(f3 a, f3 b) {
+    return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+__device__ __forceinline__ bool iszero3(f3 v) { return v.x == 0.f && v.y == 0.f && v.z == 0.f; }
+
+constexpr float kEps = 0.01f;                              // geom.h:6 EPSILON
+constexpr float kPi = 3.14159265358979323846f;             // geom.h:7 FLOAT_PI
+constexpr unsigned kRandN = BDPT_DEV_RAND_N;
+
+// sinf/cosf with correctly-rounded semantics: fp64 sincos rounded once to fp32.
+__device__ __forceinline__ void sincos_cr(float x, float* s, float* c) {
+    double sd, cd;
+    sincos((double)x, &sd, &cd);
+    *s = (float)sd;
+    *c = (float)cd;
+}
+
+// SphereIntersectDevice device.cu:80-104 (g = {p.x, p.y, p.z, rad*rad}).
+__device__ __forceinline__ float sphere_isect(float4 g, f3 o, f3 d) {
+    f3 op = mk(g.x - o.x, g.y - o.y, g.z - o.z);
+    float b = dot(op, d);
+    float det = b * b - dot(op, op) + g.w;
+    if (det < 0.f) return 0.f;
+    det = sqrtf(det);
+    float t = b - det;
+    if (t > kEps) return t;
+    t = b + det;
+    return t > kEps ? t : 0.f;
+}
+
+// UniformSampleSphereDevice device.cu:157-165
+__device__ __forceinline__ f3 uniform_sphere(float u1, float u2) {
+    const float zz = 1.f - 2.f * u1;
+    const float q = 1.f - zz * zz;
+    const float r = sqrtf(0.f > q ? 0.f : q);
+    const float phi = 2.f * kPi * u2;
+    float s, c;
+    sincos_cr(phi, &s, &c);
+    return mk(r * c, r * s, zz);
+}
+
+// Cosine-weighted direction about w (device.cu:676-699; also :190-212 and :357-380).
+__device__ __forceinline__ f3 cosine_dir(f3 w, float u_phi, float u_r2) {
+    const float r1 = 2.f * kPi * u_phi;
+    const float r2 = u_r2;
+    const float r2s = sqrtf(r2);
+    f3 a = fabsf(w.x) > .1f ? mk(0.f, 1.f, 0.f) : mk(1.f, 0.f, 0.f);
+    f3 u = norm(cross(a, w));
+    f3 v = cross(w, u);
+    float s, c;
+    sincos_cr(r1, &s, &c);
+    u = smul(c * r2s, u);
+    v = smul(s * r2s, v);
+    f3 nd = add(u, v);
+    w = smul(sqrtf(1 - r2), w);
+    return add(nd, w);
+}
+
+}  // namespace
+
+// =============================================================================================
+// Kernel 1: MT607 table (RandomGPU MersenneTwister_kernel.cu:63-110).  4096 independent twisters,
+// lane-major output d_Rand[tid + k*4096].  The 19-word state lives in VGPRs: the recurrence is
+// unrolled by its period so every state index is a compile-time constant (no scratch).
+// =============================================================================================
+template <int S>
+__device__ __forceinline__ void mt_step(unsigned (&mt)[19], unsigned a, unsigned mb, unsigned mc,
+                                        float* __restrict__ out, int tid, int k) {
+    constexpr int S1 = (S + 1) % 19, SM = (S + 9) % 19;
+    unsigned y = (mt[S] & 0xFFFFFFFEu) | (mt[S1] & 0x1u);
+    y = mt[SM] ^ (y >> 1) ^ ((y & 1u) ? a : 0u);
+    mt[S] = y;
+    y ^= y >> 12;
+    y ^= (y << 7) & mb;
+    y ^= (y << 15) & mc;
+    y ^= y >> 18;
+    if (k < BDPT_DEV_N_PER_RNG) out[tid + k * 4096] = ((float)y + 1.0f) / 4294967296.0f;
+}
+
+template <int... S>
+__device__ __forceinline__ void mt_round(unsigned (&mt)[19], unsigned a, unsigned mb, unsigned mc,
+                                         float* __restrict__ out, int tid, int k0,
+                                         std::integer_sequence<int, S...>) {
+    (mt_step<S>(mt, a, mb, mc, out, tid, k0 + S), ...);
+}
+
+extern "C" __global__ __launch_bounds__(64) void bdpt_mt607_kernel(const uint4* __restrict__ params,
+                                                                   unsigned seed,
+                                                                   float* __restrict__ out) {
+    const int tid = blockIdx.x * 64 + threadIdx.x;
+    const uint4 p = params[tid];
+    unsigned mt[19];
+    mt[0] = seed;
+#pragma unroll
+    for (int s = 1; s < 19; s++) mt[s] = 1812433253u * (mt[s - 1] ^ (mt[s - 1] >> 30)) + (unsigned)s;
+    for (int k0 = 0; k0 < BDPT_DEV_N_PER_RNG; k0 += 19)
+        mt_round(mt, p.x, p.y, p.z, out, tid, k0, std::make_integer_sequence<int, 19>{});
+}
+
+// =============================================================================================
+// Kernel 2: light pass -- GetRayKernel (device.cu:167-219) + RadianceLightTracingKernel
+// (device.cu:222-455, DEPTH = 1) for every emitter in sphere order, fused: each thread owns
+// VLP `ind` and applies the lights in the order the reference launches them (smallpt_cpu.c:311).
+// =============================================================================================
+extern "C" __global__ __launch_bounds__(64) void bdpt_light_kernel(const bdpt_dev_sphere* __restrict__ sph,
+                                                                   unsigned n,
+                                                                   const float* __restrict__ rnd,
+                                                                   int current_sample,
+                                                                   bdpt_dev_lightpath* __restrict__ lp) {
+    const int ind = blockIdx.x * 64 + threadIdx.x;
+    bdpt_dev_lightpath out = lp[ind];
+    for (unsigned li = 0; li < n; li++) {
+        const bdpt_dev_sphere L = sph[li];
+        const f3 Le = mk(L.ex, L.ey, L.ez), Lp = mk(L.px, L.py, L.pz);
+        if (iszero3(Le)) continue;
+        // GetRayKernel, seed_id = 0
+        const unsigned i = (unsigned)(current_sample * 5 + ind * 4) % (kRandN - 4u);
+        const unsigned j = i + 2;
+        const f3 usp = uniform_sphere(rnd[j], rnd[i]);
+        const f3 spt = add(smul(L.rad, usp), Lp);
+        const f3 normal = norm(sub(spt, Lp));
+        const f3 ro = spt;
+        const f3 rd = cosine_dir(normal, rnd[i + 1], rnd[j + 1]);
+        // RadianceLightTracingKernel
+        f3 thr = smul(0.25f, Le);
+        float t = 1e20f;
+        int id = -1;
+        for (int s = (int)n - 1; s >= 0; --s) {
+            const bdpt_dev_sphere& S = sph[s];
+            const float d = sphere_isect(make_float4(S.px, S.py, S.pz, S.rr), ro, rd);
+            if (d != 0.f && d < t) { t = d; id = s; }
+        }
+        if (id < 0) {                                               // escaped (:279-292)
+            const f3 nor = smul((float)(-1. / (double)L.rad), sub(ro, Lp));
+            const f3 hr = smul(0.5f, Le);
+            out.hx = ro.x; out.hy = ro.y; out.hz = ro.z;
+            out.rx = hr.x; out.ry = hr.y; out.rz = hr.z;
+            out.nx = nor.x; out.ny = nor.y; out.nz = nor.z;
+            continue;
+        }
+        const bdpt_dev_sphere O = sph[id];
+        if (!iszero3(mk(O.ex, O.ey, O.ez))) continue;              // :296-298
+        const f3 hit = add(ro, smul(t, rd));
+        const f3 nrm = norm(sub(hit, mk(O.px, O.py, O.pz)));
+        const float dp = dot(nrm, rd);
+        const f3 nl = smul(-1.f * (float)(dp > 0 ? 1 : -1), nrm);
+        if (O.refl == BDPT_DEV_DIFF) {                              // VecMultiply :10-42, store :330-337
+            const float tol = (float)0.0001;
+            float tt;
+            if (thr.x != 0.f && O.cx != 0.f) { tt = thr.x * O.cx; if (!(tt <= tol || thr.x == tt)) thr.x = tt; } else thr.x = 0.f;
+            if (thr.y != 0.f && O.cy != 0.f) { tt = thr.y * O.cy; if (!(tt <= tol || thr.y == tt)) thr.y = tt; } else thr.y = 0.f;
+            if (thr.z != 0.f && O.cz != 0.f) { tt = thr.z * O.cz; if (!(tt <= tol || thr.z == tt)) thr.z = tt; } else thr.z = 0.f;
+            out.hx = hit.x; out.hy = hit.y; out.hz = hit.z;
+            out.rx = thr.x; out.ry = thr.y; out.rz = thr.z;
+            out.nx = nl.x; out.ny = nl.y; out.nz = nl.z;
+        }
+    }
+    lp[ind] = out;
+}
+
+// =============================================================================================
+// Kernel 3: the eye-path integrator (RadiancePathTracingKernel device.cu:544-791), `npass`
+// passes fused into one launch.
+//
+//  * One lane = one pixel for the whole launch; the running mean (c*k1 + r)*k2 and the counter
+//    stay in VGPRs across passes and are written once, coalesced, at the end (36 B/pixel/launch).
+//  * Path regeneration: one loop iteration = one path segment for every live lane; a lane whose
+//    path ends accumulates and immediately starts its next pass, so lanes never idle waiting for
+//    the longest path of the wave (the reference's 1-spp launch idles them).
+//  * The sphere list is staged in LDS once per workgroup ({p, rad^2} for traversal, emission /
+//    colour / material for shading); traversal reads are wave-uniform broadcasts.
+//  * 256-thread workgroup = 16x16 pixel tile as 2x2 waves of 8x8 pixels (2-D tiles keep the
+//    paths of a wave coherent).
+// =============================================================================================
+extern "C" __global__ __launch_bounds__(256) void bdpt_path_kernel(bdpt_path_args a) {
+    extern __shared__ float4 smem[];
+    float4* G = smem;                 // {px, py, pz, rad*rad}
+    float4* E = smem + a.n;           // {ex, ey, ez, rad}
+    float4* C = smem + 2 * a.n;       // {cx, cy, cz, bits(refl | emissive<<8)}
+    float4* P = smem + 3 * a.n;       // {px, py, pz, 0} (hit normal)
+    for (unsigned s = threadIdx.x; s < a.n; s += 256) {
+        const bdpt_dev_sphere S = a.sph[s];
+        G[s] = make_float4(S.px, S.py, S.pz, S.rr);
+        E[s] = make_float4(S.ex, S.ey, S.ez, S.rad);
+        const bool emis = !(S.ex == 0.f && S.ey == 0.f && S.ez == 0.f);
+        C[s] = make_float4(S.cx, S.cy, S.cz, __int_as_float(S.refl | (emis ? 256 : 0)));
+        P[s] = make_float4(S.px, S.py, S.pz, 0.f);
+    }
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
+    const int y = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+    bool active = x < a.W && y < a.H;
+    if (active && a.nshards > 1) active = ((y / a.band_rows) % a.nshards) == a.shard;
+    if (!active) return;
+
+    const int i = y * a.W + x;
+    const unsigned ibase = 26u + (unsigned)(i * 25);
+    const float* __restrict__ rnd = a.rnd;
+
+    // running mean state (device.cu:774-787)
+    bdpt_dev_vec cv = a.colors[i];
+    f3 col = mk(cv.x, cv.y, cv.z);
+    unsigned cnt = a.counter[i];
+    const unsigned cnt0 = cnt;
+
+    // camera constants (device.cu:562-600), computed on the host with the same float ops
+    const f3 ux = mk(a.ux[0], a.ux[1], a.ux[2]);
+    const f3 uy = mk(a.uy[0], a.uy[1], a.uy[2]);
+    const f3 ud = mk(a.ud[0], a.ud[1], a.ud[2]);
+    const f3 org = mk(a.orig[0], a.orig[1], a.orig[2]);
+    const double kx0 = (double)((float)x * a.inv_w) - a.half_w;
+    const double ky0 = (double)((float)y * a.inv_h) - a.half_h;
+
+    int p = 0;
+    f3 ro = mk(0.f, 0.f, 0.f), rd = ro, thr = ro, rad = ro;
+    unsigned depth = 0, sid = 0;
+    int vlp = 0;
+    bool specular = true, fresh = true;
+
+    while (p < a.npass && cnt < BDPT_DEV_COUNTER_CAP) {
+        if (fresh) {                                                     // camera ray (:562-600)
+            sid = a.sid[p];
+            vlp = a.vlp[p] & (BDPT_DEV_LIGHT_POINTS - 1);
+            const unsigned kk = (ibase + sid) % (kRandN - 5u);
+            const float kx = (float)(kx0 + (double)(rnd[kk] * a.inv_w));
+            const float ky = (float)(ky0 + (double)(rnd[kk + 1] * a.inv_h));
+            const float kz = 10.0f;
+            f3 rdir = mk(0.f, 0.f, 0.f);
+            rdir = add(rdir, smul(kx, ux));
+            rdir = add(rdir, smul(ky, uy));
+            rdir = add(rdir, smul(kz, ud));
+            const float w = (a.tx * kx + a.ty * ky + a.tz * kz) + 1;
+            rdir = smul((float)(1. / (double)w), rdir);
+            ro = add(rdir, org);
+            rd = norm(rdir);
+            rad = mk(0.f, 0.f, 0.f);
+            thr = mk(1.f, 1.f, 1.f);
+            specular = true;
+            depth = 0;
+            fresh = false;
+        }
+        const unsigned j = (ibase + depth * 5u + sid) % (kRandN - 5u);
+
+        // closest hit, scanning from the last sphere down (device.cu:106-124)
+        float t = 1e20f;
+        int id = -1;
+        for (int s = (int)a.n - 1; s >= 0; --s) {
+            const float d = sphere_isect(G[s], ro, rd);
+            if (d != 0.f && d < t) { t = d; id = s; }
+        }
+        bool done = id < 0;
+        if (!done) {
+            const float4 cm = C[id];
+            const int mat = __float_as_int(cm.w);
+            const float4 pc = P[id];
+            const f3 hit = add(ro, smul(t, rd));
+            const f3 normal = norm(sub(hit, mk(pc.x, pc.y, pc.z)));
+            const float dp = dot(normal, rd);
+            const f3 nl = smul(-1.f * (float)(dp > 0 ? 1 : -1), normal);
+            if (mat & 256) {                                             // emitter (:651-661)
+                if (specular) {
+                    const float4 em = E[id];
+                    rad = add(rad, mul(thr, smul(fabsf(dp), mk(em.x, em.y, em.z))));
+                }
+                done = true;
+            } else if ((mat & 255) == BDPT_DEV_DIFF) {                   // :663-703
+                specular = false;
+                thr = mul(thr, mk(cm.x, cm.y, cm.z));
+                // SampleLightsDevice(.., nn = j+2) device.cu:457-542
+                f3 res = mk(0.f, 0.f, 0.f);
+                const unsigned dk = j + 3, dj = j + 4;
+                for (unsigned li = 0; li < a.n_lights; li++) {
+                    const int ls = a.lights[li];
+                    const float4 le = E[ls];
+                    const float4 lg = G[ls];
+                    const f3 usp = uniform_sphere(rnd[dk], rnd[dj]);
+                    const f3 spt = add(smul(le.w, usp), mk(lg.x, lg.y, lg.z));
+                    f3 sd = sub(spt, hit);
+                    const float len = sqrtf(dot(sd, sd));
+                    sd = smul(1.f / len, sd);
+                    float wo = dot(sd, usp);
+                    if (wo > 0.f) continue;
+                    wo = -wo;
+                    const float wi = dot(sd, nl);
+                    if (wi > 0.f) {
+                        const float maxt = len - kEps;
+                        bool occluded = false;
+                        for (int s = (int)a.n - 1; s >= 0; --s) {
+                            const float d = sphere_isect(G[s], hit, sd);
+                            if (d != 0.f && d < maxt) { occluded = true; break; }
+                        }
+                        if (!occluded) {
+                            const float sc = (4.f * kPi * le.w * le.w) * wi * wo / (len * len);
+                            res = add(res, smul(sc, mk(le.x, le.y, le.z)));
+                        }
+                    }
+                }
+                f3 vres = mk(0.f, 0.f, 0.f);
+                {
+                    const bdpt_dev_lightpath L = a.lp[vlp];
+                    f3 sd = sub(mk(L.hx, L.hy, L.hz), hit);
+                    const float len = sqrtf(dot(sd, sd));
+                    sd = smul(1.f / len, sd);
+                    float wo = dot(sd, mk(L.nx, L.ny, L.nz));
+                    if (!(wo > 0.f)) {
+                        wo = -wo;
+                        const float wi = dot(sd, nl);
+                        if (wi > 0.f) {
+                            const float maxt = len - kEps;
+                            bool occluded = false;
+                            for (int s = (int)a.n - 1; s >= 0; --s) {
+                                const float d = sphere_isect(G[s], hit, sd);
+                                if (d != 0.f && d < maxt && !(__float_as_int(C[s].w) & 256)) {
+                                    occluded = true;
+                                    break;
+                                }
+                            }
+                            if (!occluded) vres = add(vres, smul(wi * wo, mk(L.rx, L.ry, L.rz)));
+                        }
+                    }
+                }
+                vres = smul(1.f, vres);
+                res = add(res, vres);
+                res = smul(0.5f, res);
+                rad = add(rad, mul(res, thr));
+                ro = hit;
+                rd = cosine_dir(nl, rnd[j], rnd[j + 1]);
+            } else if ((mat & 255) == BDPT_DEV_SPEC) {                   // :704-714
+                specular = true;
+                const f3 nd = sub(rd, smul(2.f * dot(normal, rd), normal));
+                thr = mul(thr, mk(cm.x, cm.y, cm.z));
+                ro = hit;
+                rd = nd;
+            } else {                                                     // REFR / LITE :715-770
+                specular = true;
+                const f3 refl = sub(rd, smul(2.f * dot(normal, rd), normal));
+                const bool into = dot(normal, nl) > 0;
+                const float nc = 1.f, nt = 1.5f;
+                const float nnt = into ? nc / nt : nt / nc;
+                const float ddn = dot(rd, nl);
+                const float cos2t = 1.f - nnt * nnt * (1.f - ddn * ddn);
+                if (cos2t < 0.f) {
+                    thr = mul(thr, mk(cm.x, cm.y, cm.z));
+                    ro = hit;
+                    rd = refl;
+                } else {
+                    const float kq = (float)(into ? 1 : -1) * (ddn * nnt + sqrtf(cos2t));
+                    const f3 td = norm(sub(smul(nnt, rd), smul(kq, normal)));
+                    const float aa = nt - nc, bb = nt + nc;
+                    const float R0 = aa * aa / (bb * bb);
+                    const float c = 1 - (into ? -ddn : dot(td, normal));
+                    const float Re = R0 + (1 - R0) * c * c * c * c * c;
+                    const float Tr = 1.f - Re;
+                    const float P = .25f + .5f * Re;
+                    const float RP = Re / P;
+                    const float TP = Tr / (1.f - P);
+                    if (rnd[j + 2] < P) {
+                        thr = mul(smul(RP, thr), mk(cm.x, cm.y, cm.z));
+                        rd = refl;
+                    } else {
+                        thr = mul(smul(TP, thr), mk(cm.x, cm.y, cm.z));
+                        rd = td;
+                    }
+                    ro = hit;
+                }
+            }
+            if (!done && ++depth > 6) done = true;                       // :621 7-segment cap
+        }
+        if (done) {                                                      // :774-787
+            if (cnt == 0) {
+                col = rad;
+            } else {
+                const float k1 = (float)cnt;
+                const float k2 = 1.f / (k1 + 1.f);
+                col.x = (col.x * k1 + rad.x) * k2;
+                col.y = (col.y * k1 + rad.y) * k2;
+                col.z = (col.z * k1 + rad.z) * k2;
+            }
+            cnt++;
+            p++;
+            fresh = true;
+        }
+    }
+    if (cnt == cnt0) return;                                             // nothing rendered
+    bdpt_dev_vec out;
+    out.x = col.x; out.y = col.y; out.z = col.z;
+    a.colors[i] = out;
+    a.counter[i] = cnt;
+    a.pixels[i] = bdpt_dev_to_rgba(col.x, col.y, col.z, a.gamma_thr);
+}
+
+// Recompute pixels from colors (after a cross-GPU reduce of the radiance frame).
+extern "C" __global__ __launch_bounds__(256) void bdpt_pixels_kernel(const bdpt_dev_vec* __restrict__ colors,
+                                                                     uchar4* __restrict__ pixels,
+                                                                     const float* __restrict__ thr,
+                                                                     int count) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= count) return;
+    const bdpt_dev_vec c = colors[i];
+    pixels[i] = bdpt_dev_to_rgba(c.x, c.y, c.z, thr);
+}

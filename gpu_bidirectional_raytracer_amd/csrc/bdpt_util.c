@@ -1,0 +1,268 @@
+/*
+ * bdpt_util.c -- host-side C pieces of the drop-in that live outside the render kernels:
+ * the .scn loader, UpdateCamera, the KeyFunc/SpecialFunc camera and sphere moves, SavePPM,
+ * a glibc-compatible rand(), the reference's pass (sid / vlp_index) state machine, and the
+ * toInt threshold table the path kernel uses for its 8-bit output.
+ * Built with -ffp-contract=off: every float expression keeps the reference's rounding.
+ */
+#define _GNU_SOURCE
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../include/bdpt.h"
+
+static bdpt_vec vinit(float a, float b, float c) { bdpt_vec v; v.x = a; v.y = b; v.z = c; return v; }
+static bdpt_vec vadd(bdpt_vec a, bdpt_vec b) { return vinit(a.x + b.x, a.y + b.y, a.z + b.z); }
+static bdpt_vec vsub(bdpt_vec a, bdpt_vec b) { return vinit(a.x - b.x, a.y - b.y, a.z - b.z); }
+static bdpt_vec vsmul(float k, bdpt_vec b) { return vinit(k * b.x, k * b.y, k * b.z); }
+static float vdot(bdpt_vec a, bdpt_vec b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+static bdpt_vec vnorm(bdpt_vec v) { float l = 1.f / sqrtf(vdot(v, v)); return vsmul(l, v); }
+static bdpt_vec vxcross(bdpt_vec a, bdpt_vec b) {
+    return vinit(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+
+/* ReadScene display_func.c:112-175: same fscanf formats, same error conditions. */
+int bdpt_read_scene(const char *path, bdpt_camera *cam, bdpt_sphere **out, unsigned *n_out)
+{
+    if (!path || !cam || !out || !n_out) return BDPT_EINVAL;
+    *out = NULL;
+    *n_out = 0;
+    FILE *f = fopen(path, "r");
+    if (!f) {
+        fprintf(stderr, "Failed to open file: %s\n", path);
+        return BDPT_EIO;
+    }
+    int c = fscanf(f, "camera %f %f %f  %f %f %f\n", &cam->orig.x, &cam->orig.y, &cam->orig.z,
+                   &cam->target.x, &cam->target.y, &cam->target.z);
+    if (c != 6) {
+        fprintf(stderr, "Failed to read 6 camera parameters: %d\n", c);
+        fclose(f);
+        return BDPT_EIO;
+    }
+    unsigned n = 0;
+    c = fscanf(f, "size %u\n", &n);
+    if (c != 1) {
+        fprintf(stderr, "Failed to read sphere count: %d\n", c);
+        fclose(f);
+        return BDPT_EIO;
+    }
+    bdpt_sphere *s = (bdpt_sphere *)malloc(sizeof(bdpt_sphere) * (n ? n : 1));
+    if (!s) { fclose(f); return BDPT_ENOMEM; }
+    for (unsigned i = 0; i < n; i++) {
+        int mat = -1;
+        c = fscanf(f, "sphere %f  %f %f %f  %f %f %f  %f %f %f  %d\n", &s[i].rad, &s[i].p.x,
+                   &s[i].p.y, &s[i].p.z, &s[i].e.x, &s[i].e.y, &s[i].e.z, &s[i].c.x, &s[i].c.y,
+                   &s[i].c.z, &mat);
+        if (mat < 0 || mat > 3) {
+            fprintf(stderr, "Failed to read material type for sphere #%u: %d\n", i, mat);
+            free(s);
+            fclose(f);
+            return BDPT_EIO;
+        }
+        s[i].refl = mat;                       /* 0..3 -> DIFF, SPEC, REFR, LITE */
+        if (c != 11) {
+            fprintf(stderr, "Failed to read sphere #%u: %d\n", i, c);
+            free(s);
+            fclose(f);
+            return BDPT_EIO;
+        }
+    }
+    fclose(f);
+    *out = s;
+    *n_out = n;
+    return BDPT_OK;
+}
+
+void bdpt_free_scene(bdpt_sphere *s) { free(s); }
+
+/* CornellSpheres scene.h:7-18 and the no-argument camera smallpt_cpu.c:404-405. */
+unsigned bdpt_default_scene(bdpt_camera *cam, bdpt_sphere *s)
+{
+    const float W = 1e4f;
+    const bdpt_sphere def[9] = {
+        {W, {W + 1.f, 40.8f, 81.6f}, {0.f, 0.f, 0.f}, {.75f, .25f, .25f}, BDPT_DIFF},
+        {W, {-W + 99.f, 40.8f, 81.6f}, {0.f, 0.f, 0.f}, {.25f, .25f, .75f}, BDPT_DIFF},
+        {W, {50.f, 40.8f, W}, {0.f, 0.f, 0.f}, {.75f, .75f, .75f}, BDPT_DIFF},
+        {W, {50.f, 40.8f, -W + 270.f}, {0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}, BDPT_DIFF},
+        {W, {50.f, W, 81.6f}, {0.f, 0.f, 0.f}, {.75f, .75f, .75f}, BDPT_DIFF},
+        {W, {50.f, -W + 81.6f, 81.6f}, {0.f, 0.f, 0.f}, {.75f, .75f, .75f}, BDPT_DIFF},
+        {16.5f, {27.f, 16.5f, 47.f}, {0.f, 0.f, 0.f}, {.9f, .9f, .9f}, BDPT_SPEC},
+        {16.5f, {73.f, 16.5f, 78.f}, {0.f, 0.f, 0.f}, {.9f, .9f, .9f}, BDPT_REFR},
+        {7.f, {50.f, 81.6f - 15.f, 81.6f}, {12.f, 12.f, 12.f}, {0.f, 0.f, 0.f}, BDPT_REFR},
+    };
+    if (s) memcpy(s, def, sizeof(def));
+    if (cam) {
+        memset(cam, 0, sizeof(*cam));
+        cam->orig = vinit(50.f, 44.f, 176.f);
+        cam->target = vinit(50.f, 44 - 0.042612f, 175.f);
+    }
+    return 9;
+}
+
+/* UpdateCamera display_func.c:177-190. */
+void bdpt_update_camera(bdpt_camera *c, int width, int height)
+{
+    c->dir = vnorm(vsub(c->target, c->orig));
+    const bdpt_vec up = vinit(0.f, 1.f, 0.f);
+    const float fov = (float)((M_PI / 180.f) * 45.f);
+    c->x = vnorm(vxcross(c->dir, up));
+    c->x = vsmul(width * fov / height, c->x);
+    c->y = vnorm(vxcross(c->x, c->dir));
+    c->y = vsmul(fov, c->y);
+}
+
+#define MOVE_STEP 10.0f
+#define ROTATE_STEP (2.f * M_PI / 180.f)
+
+/* KeyFunc / SpecialFunc camera moves, display_func.c:291-334 and :386-433.  The rotations
+ * reuse the already-updated component, exactly as the reference does (survey Appendix A.9). */
+int bdpt_camera_key(bdpt_camera *c, int key)
+{
+    bdpt_vec d, t;
+    switch (key) {
+    case 'a': d = vsmul(-MOVE_STEP, vnorm(c->x)); break;
+    case 'd': d = vsmul(MOVE_STEP, vnorm(c->x)); break;
+    case 'w': d = vsmul(MOVE_STEP, c->dir); break;
+    case 's': d = vsmul(-MOVE_STEP, c->dir); break;
+    case 'r': c->orig.y += MOVE_STEP; c->target.y += MOVE_STEP; return 1;
+    case 'f': c->orig.y -= MOVE_STEP; c->target.y -= MOVE_STEP; return 1;
+    case ' ': return 1;                                  /* ReInit(1) with no move */
+    case BDPT_KEY_PAGE_UP: c->target.y += MOVE_STEP; return 1;
+    case BDPT_KEY_PAGE_DOWN: c->target.y -= MOVE_STEP; return 1;
+    case BDPT_KEY_UP:
+    case BDPT_KEY_DOWN:
+        t = vsub(c->target, c->orig);
+        {
+            const double a = key == BDPT_KEY_UP ? -ROTATE_STEP : ROTATE_STEP;
+            t.y = t.y * cos(a) + t.z * sin(a);
+            t.z = -t.y * sin(a) + t.z * cos(a);
+        }
+        c->target = vadd(t, c->orig);
+        return 1;
+    case BDPT_KEY_LEFT:
+    case BDPT_KEY_RIGHT:
+        t = vsub(c->target, c->orig);
+        {
+            const double a = key == BDPT_KEY_LEFT ? -ROTATE_STEP : ROTATE_STEP;
+            t.x = t.x * cos(a) - t.z * sin(a);
+            t.z = t.x * sin(a) + t.z * cos(a);
+        }
+        c->target = vadd(t, c->orig);
+        return 1;
+    default:
+        return 0;
+    }
+    /* vsmul(direction, +-MOVE_STEP, direction); vadd(orig, orig, direction); vadd(target, ...) */
+    c->orig = vadd(c->orig, d);
+    c->target = vadd(c->target, d);
+    return 1;
+}
+
+/* KeyFunc sphere edits display_func.c:347-370 (0.5f * MOVE_STEP along one axis). */
+int bdpt_sphere_key(bdpt_sphere *s, unsigned n, int cur, int key)
+{
+    if (!s || cur < 0 || (unsigned)cur >= n) return 0;
+    switch (key) {
+    case '4': s[cur].p.x -= 0.5f * MOVE_STEP; return 1;
+    case '6': s[cur].p.x += 0.5f * MOVE_STEP; return 1;
+    case '8': s[cur].p.z -= 0.5f * MOVE_STEP; return 1;
+    case '2': s[cur].p.z += 0.5f * MOVE_STEP; return 1;
+    case '9': s[cur].p.y += 0.5f * MOVE_STEP; return 1;
+    case '3': s[cur].p.y -= 0.5f * MOVE_STEP; return 1;
+    default: return 0;
+    }
+}
+
+/* SavePPM smallpt_cpu.c:239-262: "P3\n%d %d\n%d\n", rows bottom-up, "%d %d %d " per pixel. */
+int bdpt_save_ppm(const char *path, const unsigned char *rgba, int w, int h)
+{
+    if (!path || !rgba || w <= 0 || h <= 0) return BDPT_EINVAL;
+    FILE *f = fopen(path, "w");
+    if (!f) {
+        fprintf(stderr, "Failed to open image file: %s\n", path);
+        return BDPT_EIO;
+    }
+    fprintf(f, "P3\n%d %d\n%d\n", w, h, 255);
+    for (int y = h - 1; y >= 0; --y) {
+        const unsigned char *p = rgba + 4 * (size_t)y * w;
+        for (int x = 0; x < w; ++x, p += 4) fprintf(f, "%d %d %d ", p[0], p[1], p[2]);
+    }
+    return fclose(f) == 0 ? BDPT_OK : BDPT_EIO;
+}
+
+/* glibc random_r TYPE_3 (x**31 + x**3 + 1), the generator behind rand(). */
+void bdpt_srand(bdpt_rand_state *st, unsigned seed)
+{
+    int *r = st->state;
+    if (seed == 0) seed = 1;
+    r[0] = (int)seed;
+    long word = (long)(int)seed;
+    for (int i = 1; i < 31; i++) {
+        long hi = word / 127773, lo = word % 127773;
+        word = 16807 * lo - 2836 * hi;
+        if (word < 0) word += 2147483647;
+        r[i] = (int)word;
+    }
+    st->f = 3;
+    st->r = 0;
+    for (int i = 0; i < 310; i++) (void)bdpt_rand(st);
+}
+
+int bdpt_rand(bdpt_rand_state *st)
+{
+    int *r = st->state;
+    unsigned val = (unsigned)r[st->f] + (unsigned)r[st->r];
+    r[st->f] = (int)val;
+    if (++st->f >= 31) { st->f = 0; ++st->r; }
+    else if (++st->r >= 31) st->r = 0;
+    return (int)(val >> 1);
+}
+
+void bdpt_pass_state_init(bdpt_pass_state *ps)
+{
+    bdpt_srand(&ps->rng, 1);                     /* rand() never seeded: seed 1 */
+    ps->flag = 1;                                /* display_func.c:44 */
+    ps->vlp_index = 1;                           /* smallpt_cpu.c:47 MAX_VLP */
+}
+
+void bdpt_pass_state_light(bdpt_pass_state *ps) { ps->flag = 2; }   /* smallpt_cpu.c:361 */
+
+void bdpt_pass_state_next(bdpt_pass_state *ps, unsigned *sid, int *vlp)
+{
+    *sid = (unsigned)bdpt_rand(&ps->rng) % (unsigned)BDPT_RAND_N;        /* :270 */
+    *vlp = ps->vlp_index % BDPT_LIGHT_POINTS;
+    if (ps->flag == 3) { ps->vlp_index += 1; ps->flag = 1; }            /* :292 MAX_ITER=3 */
+    if (ps->flag < 3) ps->flag++;                                        /* :293 */
+}
+
+void bdpt_pass_schedule(bdpt_pass_state *ps, int npass, unsigned *sid, int *vlp)
+{
+    for (int p = 0; p < npass; p++) bdpt_pass_state_next(ps, &sid[p], &vlp[p]);
+}
+
+/* toInt vec.h:34 with correctly-rounded powf semantics.  thr[k] (k = 1..255) is the smallest
+ * non-negative float x with toInt(x) >= k; toInt is monotone, so the kernel's count of
+ * thresholds <= x equals toInt(x) for every float (NaN and negatives give 0). thr[0] = -inf. */
+static int to_int_ref(float x)
+{
+    float c = x < 0.f ? 0.f : (x > 1.f ? 1.f : x);
+    float pw = (float)pow((double)c, (double)(1.f / 2.2f));
+    return (int)(pw * 255.f + .5f);
+}
+
+void bdpt_gamma_thresholds(float thr[256])
+{
+    thr[0] = -INFINITY;
+    for (int k = 1; k < 256; k++) {
+        unsigned lo = 0, hi = 0x3f800000u;          /* toInt(1.0f) = 255 >= k */
+        while (lo < hi) {
+            unsigned mid = lo + (hi - lo) / 2;
+            float x;
+            memcpy(&x, &mid, 4);
+            if (to_int_ref(x) >= k) hi = mid; else lo = mid + 1;
+        }
+        memcpy(&thr[k], &lo, 4);
+    }
+}

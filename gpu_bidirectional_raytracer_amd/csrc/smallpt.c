@@ -1,0 +1,182 @@
+/*
+ * smallpt.c -- headless C host of the MI355X path tracer: the drop-in for the reference's
+ * src/smallpt_cpu.c main()/UpdateRendering*()/ReInit*() and the IdleFunc/KeyFunc loop of
+ * src/display_func.c, with GLUT replaced by a scripted key sequence.
+ *
+ *   smallpt [<width> <height> <scene.scn>] [--spp N] [--batch B] [--keys KEYS] [--out F.ppm]
+ *           [--device D] [--dat PATH]
+ *
+ * Without positional arguments the built-in CornellSpheres scene is used (smallpt_cpu.c:400).
+ * Like the reference, width/height get +1 (smallpt_cpu.c:409-410).  The first frame runs the
+ * light pass (UpdateRendering2) and then path passes; N passes are fused into launches of B.
+ * KEYS replays KeyFunc/SpecialFunc: a d w s r f (camera moves), ' ' (re-init), + - (select
+ * sphere), 4 6 8 2 9 3 (move the selected sphere), U D L R (arrow keys), P/p (PageUp/Down
+ * targets -> here 'P' = PageUp, 'Q' = PageDown); after each key N more passes are rendered.
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/time.h>
+
+#include "../../include/bdpt.h"
+
+static double wall_clock(void)                            /* WallClockTime display_func.c:61 */
+{
+    struct timeval t;
+    gettimeofday(&t, NULL);
+    return t.tv_sec + t.tv_usec / 1000000.0;
+}
+
+typedef struct {
+    bdpt_ctx *ctx;
+    bdpt_camera camera;
+    bdpt_sphere *spheres;
+    unsigned n;
+    int width, height;
+    int current_sample, reinit_counter, current_sphere;
+    float total_time;
+    bdpt_pass_state ps;
+} host;
+
+static void report(host *h, int rc, const char *what)
+{
+    if (rc != BDPT_OK) fprintf(stderr, "%s failed: %s\n", what, bdpt_last_error(h->ctx));
+}
+
+/* UpdateRendering2 smallpt_cpu.c:300-362 */
+static void update_rendering2(host *h)
+{
+    printf("UpdateRendering2\n");
+    report(h, bdpt_light_pass(h->ctx, h->current_sample), "Kernel Light Tracing");
+    bdpt_pass_state_light(&h->ps);
+}
+
+/* npass x UpdateRendering smallpt_cpu.c:265-297, fused into one launch */
+static void update_rendering(host *h, int npass)
+{
+    unsigned *sid = malloc(sizeof(unsigned) * npass);
+    int *vlp = malloc(sizeof(int) * npass);
+    bdpt_pass_schedule(&h->ps, npass, sid, vlp);
+    double start = wall_clock();
+    int rc = bdpt_path_passes(h->ctx, sid, vlp, npass);
+    if (rc == BDPT_OK) rc = bdpt_synchronize(h->ctx);
+    report(h, rc, "Kernel RadiancePathTracing");
+    h->current_sample += npass;
+    const float elapsed = (float)(wall_clock() - start);
+    h->total_time += elapsed;
+    const float sample_sec = (float)h->height * h->width * npass / elapsed;
+    printf("Rendering time %.3f sec (pass %d) Total:%.2f  Sample/sec  %.1fK\n", elapsed,
+           h->current_sample, h->total_time, sample_sec / 1000.f);
+    free(sid);
+    free(vlp);
+}
+
+/* ReInit smallpt_cpu.c:373-387 (buffers persist; only the accumulation restarts) */
+static void reinit(host *h)
+{
+    report(h, bdpt_reset_accum(h->ctx), "ReInit");
+    h->reinit_counter++;
+    bdpt_update_camera(&h->camera, h->width, h->height);
+    report(h, bdpt_set_camera(h->ctx, &h->camera), "ReInit camera");
+    h->current_sample = 0;
+    if (h->reinit_counter % 2 == 0) update_rendering2(h);
+    update_rendering(h, 1);
+}
+
+/* ReInitScene smallpt_cpu.c:365-371 */
+static void reinit_scene(host *h)
+{
+    h->current_sample = 0;
+    report(h, bdpt_reset_accum(h->ctx), "ReInitScene");
+    report(h, bdpt_set_scene(h->ctx, h->spheres, h->n), "ReInitScene upload");
+    update_rendering2(h);
+}
+
+static void key(host *h, int k)
+{
+    int code = k;
+    if (k == 'U') code = BDPT_KEY_UP;
+    else if (k == 'D') code = BDPT_KEY_DOWN;
+    else if (k == 'L') code = BDPT_KEY_LEFT;
+    else if (k == 'R') code = BDPT_KEY_RIGHT;
+    else if (k == 'P') code = BDPT_KEY_PAGE_UP;
+    else if (k == 'Q') code = BDPT_KEY_PAGE_DOWN;
+    if (k == '+' || k == '-') {
+        h->current_sphere = k == '+' ? (h->current_sphere + 1) % (int)h->n
+                                     : (h->current_sphere + ((int)h->n - 1)) % (int)h->n;
+        fprintf(stderr, "Selected sphere %d (%f %f %f)\n", h->current_sphere,
+                h->spheres[h->current_sphere].p.x, h->spheres[h->current_sphere].p.y,
+                h->spheres[h->current_sphere].p.z);
+        reinit_scene(h);
+    } else if (bdpt_sphere_key(h->spheres, h->n, h->current_sphere, k)) {
+        reinit_scene(h);
+    } else if (bdpt_camera_key(&h->camera, code)) {
+        reinit(h);
+    }
+}
+
+int main(int argc, char **argv)
+{
+    host h;
+    memset(&h, 0, sizeof(h));
+    int spp = 16, batch = 64, device = 0, npos = 0;
+    const char *pos[3] = {0, 0, 0}, *out = NULL, *keys = "", *dat = "assets/data/MersenneTwister.dat";
+    for (int a = 1; a < argc; a++) {
+        if (!strcmp(argv[a], "--spp") && a + 1 < argc) spp = atoi(argv[++a]);
+        else if (!strcmp(argv[a], "--batch") && a + 1 < argc) batch = atoi(argv[++a]);
+        else if (!strcmp(argv[a], "--keys") && a + 1 < argc) keys = argv[++a];
+        else if (!strcmp(argv[a], "--out") && a + 1 < argc) out = argv[++a];
+        else if (!strcmp(argv[a], "--device") && a + 1 < argc) device = atoi(argv[++a]);
+        else if (!strcmp(argv[a], "--dat") && a + 1 < argc) dat = argv[++a];
+        else if (npos < 3) pos[npos++] = argv[a];
+        else { fprintf(stderr, "Usage: %s <window width> <window height> <scene file>\n", argv[0]); return -1; }
+    }
+    fprintf(stderr, "Usage: %s\n", argv[0]);
+    fprintf(stderr, "Usage: %s <window width> <window height> <scene file>\n", argv[0]);
+    if (npos == 3) {
+        h.width = atoi(pos[0]);
+        h.height = atoi(pos[1]);
+        fprintf(stderr, "Reading scene: %s\n", pos[2]);
+        if (bdpt_read_scene(pos[2], &h.camera, &h.spheres, &h.n) != BDPT_OK) exit(-1);
+        fprintf(stderr, "Scene size: %u\n", h.n);
+    } else if (npos == 0) {
+        h.width = 640;                                   /* display_func.c:50-52 defaults */
+        h.height = 480;
+        h.spheres = malloc(sizeof(bdpt_sphere) * 9);
+        h.n = bdpt_default_scene(&h.camera, h.spheres);
+    } else {
+        exit(-1);
+    }
+    h.height += 1;
+    h.width += 1;
+    bdpt_update_camera(&h.camera, h.width, h.height);
+    bdpt_pass_state_init(&h.ps);
+
+    fprintf(stderr, "Allocate Buffers\n");
+    int rc = bdpt_create(&h.ctx, h.spheres, h.n, h.width, h.height, dat, device);
+    if (rc != BDPT_OK) {
+        fprintf(stderr, "Unable to allocate GPU data: %s\n", bdpt_create_error());
+        return 1;
+    }
+    report(&h, bdpt_set_camera(h.ctx, &h.camera), "camera");
+
+    /* IdleFunc display_func.c:192-217: frame 1 = light pass then path pass; then path passes */
+    update_rendering2(&h);
+    for (int done = 0; done < spp; done += batch)
+        update_rendering(&h, spp - done < batch ? spp - done : batch);
+    for (const char *k = keys; *k; k++) {
+        key(&h, (unsigned char)*k);
+        for (int done = 0; done < spp; done += batch)
+            update_rendering(&h, spp - done < batch ? spp - done : batch);
+    }
+    if (out) {                                            /* SavePPM smallpt_cpu.c:239 */
+        unsigned char *rgba = malloc(4 * (size_t)h.width * h.height);
+        rc = bdpt_read_pixels(h.ctx, rgba);
+        if (rc == BDPT_OK) rc = bdpt_save_ppm(out, rgba, h.width, h.height);
+        report(&h, rc, "SavePPM");
+        free(rgba);
+    }
+    bdpt_destroy(h.ctx);
+    if (npos == 3) bdpt_free_scene(h.spheres); else free(h.spheres);
+    return rc == BDPT_OK ? 0 : 1;
+}

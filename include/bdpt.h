@@ -1,0 +1,156 @@
+/*
+ * bdpt.h -- C-ABI of the MI355X bidirectional path tracer (libbdpt.so).
+ *
+ * This is the drop-in boundary for the render path of sim186/gpu_bidirectional_raytracer.
+ * In the reference the boundary is the set of module globals plus <<<>>> launches inside
+ * src/smallpt_cpu.c; every entry point below names the reference function it replaces.
+ * Plain C: no torch / HIP types in any signature.  All functions return 0 on success and a
+ * negative BDPT_E* code on failure; the message is in bdpt_last_error() (the reference prints
+ * cudaGetErrorString() and continues, smallpt_cpu.c:169-233 -- the host does the same with this).
+ *
+ * Types are layout-compatible with the reference headers (static-asserted in the library):
+ *   bdpt_vec       == Vec        include/vec.h:4-6       (12 B)
+ *   bdpt_ray       == Ray        include/geom.h:9-11     (24 B)
+ *   bdpt_sphere    == Sphere     include/geom.h:23-27    (44 B, enum Refl stored as int)
+ *   bdpt_lightpath == LightPath  include/geom.h:29-33    (36 B)
+ *   bdpt_camera    == Camera     include/camera.h:7-12   (60 B)
+ */
+#ifndef BDPT_H
+#define BDPT_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct { float x, y, z; } bdpt_vec;
+typedef struct { bdpt_vec o, d; } bdpt_ray;
+enum { BDPT_DIFF = 0, BDPT_SPEC = 1, BDPT_REFR = 2, BDPT_LITE = 3 }; /* geom.h:18-20 enum Refl */
+typedef struct { float rad; bdpt_vec p, e, c; int refl; } bdpt_sphere;
+typedef struct { bdpt_vec hp, rad, nl; } bdpt_lightpath;
+typedef struct { bdpt_vec orig, target, dir, x, y; } bdpt_camera;
+
+/* Compile-time constants of the reference (cons.h, geom.h, smallpt_cpu.c:67-69). */
+#define BDPT_MT_RNG_COUNT 4096              /* MersenneTwister.h:28                         */
+#define BDPT_N_PER_RNG    1876              /* AlignUp(DivideRoundUp(7680000,4096),2)       */
+#define BDPT_RAND_N       (4096 * 1876)     /* 7,684,096 floats = 30.7 MB                   */
+#define BDPT_LIGHT_POINTS 4096              /* geom.h:15 LIGHT_POINTS (DEPTH=1, MAX_VLP=1)  */
+#define BDPT_MAX_SEGMENTS 7                 /* device.cu:621 `depth > 6` break               */
+#define BDPT_COUNTER_CAP  30000u            /* device.cu:607 `counter[i] < 30000`            */
+
+/* Error codes. */
+#define BDPT_OK        0
+#define BDPT_EINVAL   -1   /* bad argument                                   */
+#define BDPT_EIO      -2   /* file could not be read / written               */
+#define BDPT_EHIP     -3   /* HIP runtime error                              */
+#define BDPT_ENOMEM   -4   /* allocation failed                              */
+#define BDPT_ESTATE   -5   /* call out of order (e.g. path pass before RNG)  */
+
+typedef struct bdpt_ctx bdpt_ctx;
+
+/* ---- render-path context (replaces smallpt_cpu.c module globals + AllocateBuffers) ---- */
+
+/* AllocateBuffers smallpt_cpu.c:153-237 + loadMTGPU MersenneTwister_kernel.cu:23-36.
+ * W,H are the internal sizes AFTER the reference's +1 (smallpt_cpu.c:409-410).
+ * `device` is the HIP ordinal this context renders on. Accumulation starts zeroed. */
+int  bdpt_create(bdpt_ctx **out, const bdpt_sphere *spheres, unsigned n_spheres,
+                 int width, int height, const char *mt_dat_path, int device);
+/* FreeBuffers smallpt_cpu.c:98-110. */
+void bdpt_destroy(bdpt_ctx *ctx);
+const char *bdpt_last_error(const bdpt_ctx *ctx);
+/* Message of the last failed bdpt_create (no context exists then). */
+const char *bdpt_create_error(void);
+
+/* ReInitScene smallpt_cpu.c:365-371 (re-upload of dev_spheres, :229). Does not run the light pass. */
+int  bdpt_set_scene(bdpt_ctx *ctx, const bdpt_sphere *spheres, unsigned n_spheres);
+/* Camera by value, as RadiancePathTracingKernel receives it (device.cu:548). Call after
+ * bdpt_update_camera(). */
+int  bdpt_set_camera(bdpt_ctx *ctx, const bdpt_camera *camera);
+/* counter[] := 0 (ReInit -> AllocateBuffers, smallpt_cpu.c:204); colors/pixels follow on the
+ * next pass because counter==0 assigns (device.cu:774). */
+int  bdpt_reset_accum(bdpt_ctx *ctx);
+/* Multi-GPU sharding: only pixels whose row band (y / band_rows) % nshards == shard are
+ * rendered; all other pixels stay zero so a sum-reduce of the frames is exact. Default 0,1,*. */
+int  bdpt_set_shard(bdpt_ctx *ctx, int shard, int nshards, int band_rows);
+
+/* UpdateRendering2 smallpt_cpu.c:300-362: for every emitter in sphere order,
+ * seedMTGPU(current_sample*5) + RandomGPU (MT607 table), GetRayKernel and
+ * RadianceLightTracingKernel (4096 VLPs). */
+int  bdpt_light_pass(bdpt_ctx *ctx, int current_sample);
+/* Just the MT607 table: seedMTGPU(seed) + RandomGPU<<<32,128>>> (MersenneTwister_kernel.cu:39-110). */
+int  bdpt_generate_rand(bdpt_ctx *ctx, unsigned seed);
+
+/* `npass` x UpdateRendering (smallpt_cpu.c:265-297) fused into one launch: pass p uses
+ * sid[p] (= rand()%RAND_N, :270) and vlp_index[p] (the :292-293 state machine).
+ * Asynchronous on the context's stream; bdpt_synchronize() waits. */
+int  bdpt_path_passes(bdpt_ctx *ctx, const unsigned *sid, const int *vlp_index, int npass);
+int  bdpt_synchronize(bdpt_ctx *ctx);
+/* Device time (ms, HIP events on the context's stream) of the last bdpt_path_passes call. */
+int  bdpt_last_path_ms(bdpt_ctx *ctx, float *ms);
+/* Accumulated device time and kernel-launch count of all path-pass calls since the last reset
+ * (synchronises first).  reset != 0 zeroes the accumulators after reading them. */
+int  bdpt_path_timing(bdpt_ctx *ctx, double *total_ms, long long *launches, int reset);
+
+/* Read-back.  colors/counter: the float parity artefact (dev_colors / dev_counter);
+ * pixels: uchar4 RGBA = pixels_buf (SavePPM, smallpt_cpu.c:241). */
+int  bdpt_read_radiance(bdpt_ctx *ctx, bdpt_vec *colors, unsigned *counter);
+int  bdpt_read_pixels(bdpt_ctx *ctx, unsigned char *rgba);
+int  bdpt_read_rand(bdpt_ctx *ctx, float *rand_table);          /* d_Rand, BDPT_RAND_N */
+int  bdpt_read_lightpaths(bdpt_ctx *ctx, bdpt_lightpath *lp);   /* dev_lp, 4096        */
+/* Device pointers for zero-copy collectives (RCCL reduce of the radiance frame). */
+int  bdpt_device_buffers(bdpt_ctx *ctx, void **colors, void **counter, void **pixels);
+/* Recompute pixels (toInt gamma) from colors on the device, e.g. after a cross-GPU reduce. */
+int  bdpt_update_pixels(bdpt_ctx *ctx);
+
+/* ---- host utilities kept for the drop-in (display_func.c / smallpt_cpu.c) ---- */
+
+/* ReadScene display_func.c:112-175. *spheres is malloc'd; free with bdpt_free_scene. */
+int  bdpt_read_scene(const char *path, bdpt_camera *camera, bdpt_sphere **spheres,
+                     unsigned *n_spheres);
+void bdpt_free_scene(bdpt_sphere *spheres);
+/* The built-in CornellSpheres scene (scene.h:7-18) and camera (smallpt_cpu.c:404-405),
+ * used when the host is started without arguments. Returns the sphere count (9). */
+unsigned bdpt_default_scene(bdpt_camera *camera, bdpt_sphere *spheres_out /* >= 9 */);
+/* UpdateCamera display_func.c:177-190 (width/height are the internal sizes). */
+void bdpt_update_camera(bdpt_camera *camera, int width, int height);
+/* Camera moves of KeyFunc / SpecialFunc (display_func.c:278-437), headless.
+ * key: 'a','d','w','s','r','f' or BDPT_KEY_*; returns 1 if the camera moved (caller then
+ * does ReInit), 0 for keys that do not move the camera. */
+#define BDPT_KEY_UP        0x101
+#define BDPT_KEY_DOWN      0x102
+#define BDPT_KEY_LEFT      0x103
+#define BDPT_KEY_RIGHT     0x104
+#define BDPT_KEY_PAGE_UP   0x105
+#define BDPT_KEY_PAGE_DOWN 0x106
+int  bdpt_camera_key(bdpt_camera *camera, int key);
+/* Sphere edits of KeyFunc ('4','6','8','2','9','3': display_func.c:347-370). Returns 1 if moved. */
+int  bdpt_sphere_key(bdpt_sphere *spheres, unsigned n_spheres, int current_sphere, int key);
+/* SavePPM smallpt_cpu.c:239-262: ASCII P3, rows written bottom-up. */
+int  bdpt_save_ppm(const char *path, const unsigned char *rgba, int width, int height);
+/* The 256 thresholds behind the kernel's toInt (vec.h:34): thr[k] = smallest float whose
+ * toInt is >= k (thr[0] = -inf), with correctly-rounded powf semantics. */
+void bdpt_gamma_thresholds(float thr[256]);
+/* glibc-compatible rand()/srand() (TYPE_3 additive feedback, 31-word state), so the sid
+ * sequence `rand() % RAND_N` (smallpt_cpu.c:270, never srand'd => seed 1) is reproducible
+ * independently of the C library in use. */
+typedef struct { int state[31]; int f, r; } bdpt_rand_state;
+void bdpt_srand(bdpt_rand_state *st, unsigned seed);
+int  bdpt_rand(bdpt_rand_state *st);
+
+/* The pass scheduler of the reference: glibc rand() for sid (smallpt_cpu.c:270) and the
+ * flag / vlp_index state machine (smallpt_cpu.c:47,292-293,361; display_func.c:44,204-210).
+ * Initial state = program start: srand(1), flag = 1, vlp_index = MAX_VLP = 1. */
+typedef struct { bdpt_rand_state rng; int flag; int vlp_index; } bdpt_pass_state;
+void bdpt_pass_state_init(bdpt_pass_state *ps);
+/* UpdateRendering2 epilogue: flag = 2 (smallpt_cpu.c:361). */
+void bdpt_pass_state_light(bdpt_pass_state *ps);
+/* One UpdateRendering: returns the pass's sid and vlp_index, then applies :292-293.
+ * vlp_index is reported modulo LIGHT_POINTS (the reference reads dev_lp out of bounds once it
+ * reaches 4096 at ~8191 spp -- survey Appendix A.3; wrapping is the documented fix). */
+void bdpt_pass_state_next(bdpt_pass_state *ps, unsigned *sid, int *vlp_index);
+/* `npass` consecutive bdpt_pass_state_next calls. */
+void bdpt_pass_schedule(bdpt_pass_state *ps, int npass, unsigned *sid, int *vlp_index);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BDPT_H */

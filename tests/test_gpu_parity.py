@@ -1,0 +1,241 @@
+"""HIP kernels (through the C-ABI) vs the CPU oracle and the committed fixtures.
+
+Bar: bit-exact for the MT607 table, the VLPs, the running-mean radiance, the counters and the
+8-bit pixels on the same seeded inputs (both sides use one floating-point contract, see
+DESIGN.md).  At full size (1080p) the checks are size-independent properties plus bit-exact
+oracle rows.  The north-star tolerance (per-channel L-inf < 1e-3 after 1024 spp) is asserted too.
+"""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import gpu_bidirectional_raytracer_amd as g
+import oracle
+from conftest import GOLDEN, REPO, SCENES
+
+pytestmark = pytest.mark.gpu
+
+META = json.load(open(os.path.join(GOLDEN, "render_meta.json")))
+
+
+@pytest.fixture(scope="module")
+def rnd0():
+    return oracle.mt607(0)
+
+
+def scene(name):
+    if name == "default":
+        return g.default_scene()
+    return g.read_scene(os.path.join(SCENES, name + ".scn"))
+
+
+def make(name, W, H, gpu, light=True):
+    cam, sp = scene(name)
+    g.update_camera(cam, W, H)
+    r = g.Renderer(sp, W, H, cam, device=gpu)
+    if light:
+        r.light_pass(0)
+    return r, cam, sp
+
+
+def schedule(npass):
+    s = g.PassScheduler()
+    s.light()
+    return s.next(npass)
+
+
+def assert_same(got, ref, what):
+    if not np.array_equal(got, ref):
+        bad = np.argwhere(got != ref)
+        diff = np.abs(got.astype(np.float64) - ref.astype(np.float64))
+        raise AssertionError(f"{what}: {len(bad)} mismatches of {got.size}, first {bad[:5].tolist()}, "
+                             f"max |diff| {diff.max()}")
+
+
+def test_mt607_table_bit_exact(gpu, rnd0):
+    r, _, _ = make("cornell", 17, 9, gpu, light=False)
+    ka = json.load(open(os.path.join(GOLDEN, "known_answers.json")))
+    r.generate_rand(0)
+    t = r.read_rand()
+    assert_same(t, rnd0, "d_Rand seed 0")
+    for k, v in ka["d_rand_seed0"].items():
+        assert t[int(k)] == np.float32(v)
+    r.generate_rand(5)
+    assert_same(r.read_rand(), oracle.mt607(5), "d_Rand seed 5")
+    r.close()
+
+
+@pytest.mark.parametrize("name", ["cornell", "cornell_glass", "caustic", "simple", "cornell_2luci",
+                                  "default", "cornell_multi", "hall_of_mirrors", "complex"])
+def test_light_pass_bit_exact(gpu, rnd0, name):
+    r, cam, sp = make(name, 17, 9, gpu)
+    ref = oracle.light_pass(sp, rnd0, 0)
+    got = r.read_lightpaths()
+    assert_same(got.view(np.float32), ref.view(np.float32), f"dev_lp {name}")
+    r.close()
+
+
+@pytest.mark.parametrize("name", META["scenes"])
+def test_render_matches_golden_fixture(gpu, name):
+    W, H = META["internal_size"]
+    fx = np.load(os.path.join(GOLDEN, f"render_{name}.npz"))
+    r, cam, sp = make(name, W, H, gpu)
+    assert_same(r.read_lightpaths().view(np.float32).reshape(-1, 9), fx["lp"], "lp")
+    r.path_passes(META["sid"], META["vlp"])
+    col, cnt = r.read_radiance()
+    assert_same(col, fx["colors"], f"colors {name}")
+    assert_same(cnt, fx["counter"], f"counter {name}")
+    assert_same(r.read_pixels(), fx["pixels"], f"pixels {name}")
+    r.close()
+
+
+@pytest.mark.parametrize("name,W,H,npass", [
+    ("cornell", 61, 45, 24), ("cornell_glass", 53, 37, 24), ("caustic", 47, 35, 24),
+    ("simple", 65, 33, 24), ("default", 33, 17, 16), ("cornell_2luci", 29, 21, 16),
+    ("cornell_multi", 31, 23, 8), ("hall_of_mirrors", 31, 23, 8), ("gantz", 31, 23, 8),
+    ("cornell_mirror_reflect", 25, 19, 8), ("complex", 17, 13, 2), ("mod_cornell", 13, 11, 2),
+    ("open", 23, 17, 8), ("cornell", 1, 1, 5), ("simple", 16, 16, 3),
+])
+def test_path_passes_bit_exact(gpu, rnd0, name, W, H, npass):
+    r, cam, sp = make(name, W, H, gpu)
+    sid, vlp = schedule(npass)
+    r.path_passes(sid, vlp)
+    col, cnt = r.read_radiance()
+    lp = oracle.light_pass(sp, rnd0, 0)
+    ocol, ocnt, opx = oracle.path_passes(sp, rnd0, cam, W, H, lp, sid, vlp)
+    assert_same(cnt, ocnt, "counter")
+    assert_same(col, ocol, f"colors {name}")
+    assert_same(r.read_pixels(), opx, "pixels")
+    r.close()
+
+
+def test_split_launches_equal_one_launch(gpu):
+    sid, vlp = schedule(9)
+    a, _, _ = make("cornell", 40, 24, gpu)
+    a.path_passes(sid, vlp)
+    b, _, _ = make("cornell", 40, 24, gpu)
+    b.path_passes(sid[:2], vlp[:2])
+    b.path_passes(sid[2:7], vlp[2:7])
+    b.path_passes(sid[7:], vlp[7:])
+    for x, y in zip(a.read_radiance(), b.read_radiance()):
+        assert_same(x, y, "split")
+    a.close(); b.close()
+
+
+def test_shards_sum_to_full_frame(gpu):
+    sid, vlp = schedule(4)
+    full, _, _ = make("cornell_glass", 45, 70, gpu)
+    full.path_passes(sid, vlp)
+    fc, fn = full.read_radiance()
+    acc_c, acc_n = np.zeros_like(fc), np.zeros_like(fn)
+    for s in range(3):
+        r, _, _ = make("cornell_glass", 45, 70, gpu)
+        r.set_shard(s, 3, 16)
+        r.path_passes(sid, vlp)
+        c, n = r.read_radiance()
+        owned = ((np.arange(70) // 16) % 3 == s)
+        assert (n[~owned] == 0).all() and (n[owned] == 4).all()
+        acc_c += c
+        acc_n += n
+        r.close()
+    assert_same(acc_c, fc, "shard sum colors")
+    assert_same(acc_n, fn, "shard sum counter")
+    full.close()
+
+
+def test_reset_accum_and_scene_edit(gpu, rnd0):
+    """ReInit / ReInitScene semantics: counter restarts, new spheres, new light pass."""
+    W, H = 31, 21
+    r, cam, sp = make("cornell", W, H, gpu)
+    sid, vlp = schedule(6)
+    r.path_passes(sid[:3], vlp[:3])
+    r.reset_accum()
+    sp2 = sp.copy()
+    assert g.sphere_key(sp2, 6, "4")
+    r.set_scene(sp2)
+    r.light_pass(0)
+    r.path_passes(sid[3:], vlp[3:])
+    col, cnt = r.read_radiance()
+    lp = oracle.light_pass(sp2, rnd0, 0)
+    ocol, ocnt, _ = oracle.path_passes(sp2, rnd0, cam, W, H, lp, sid[3:], vlp[3:])
+    assert_same(cnt, ocnt, "counter after reset")
+    assert_same(col, ocol, "colors after reset")
+    r.close()
+
+
+def test_counter_cap_30000(gpu, rnd0):
+    W, H = 3, 2
+    r, cam, sp = make("simple", W, H, gpu)
+    sid, vlp = schedule(30004)
+    r.path_passes(sid, vlp)
+    col, cnt = r.read_radiance()
+    assert (cnt == 30000).all()
+    lp = oracle.light_pass(sp, rnd0, 0)
+    ocol, ocnt, _ = oracle.path_passes(sp, rnd0, cam, W, H, lp, sid, vlp)
+    assert_same(col, ocol, "colors at cap")
+    r.close()
+
+
+def test_1080p_properties_and_oracle_rows(gpu, rnd0):
+    """configs[*] at full size: counters, finiteness, pixel = toInt(colors), oracle rows."""
+    W, H, npass = 1921, 1081, 3
+    r, cam, sp = make("cornell", W, H, gpu)
+    sid, vlp = schedule(npass)
+    r.path_passes(sid, vlp)
+    col, cnt = r.read_radiance()
+    px = r.read_pixels()
+    assert (cnt == npass).all()
+    assert np.isfinite(col).all() and (col >= 0).all()
+    assert (px[..., 3] == 0).all()
+    thr = np.zeros(256, np.float32)
+    g._lib.lib.bdpt_gamma_thresholds(g._lib.ctypes.c_void_p(thr.ctypes.data))
+    k = np.searchsorted(thr, col.reshape(-1), side="right").reshape(col.shape) - 1
+    assert_same(px[..., :3], k.astype(np.uint8), "pixels vs toInt(colors)")
+    lp = oracle.light_pass(sp, rnd0, 0)
+    for y in (0, 1, 540, 1079, 1080):
+        ocol, ocnt, _ = oracle.path_passes(sp, rnd0, cam, W, H, lp, sid, vlp, rows=(y, y + 1))
+        assert_same(col[y], ocol[y], f"row {y}")
+    r.close()
+
+
+def test_linf_after_1024_spp(gpu, rnd0):
+    """North-star tolerance: per-channel L-inf < 1e-3 vs the CPU path after 1024 spp."""
+    W, H, npass = 24, 18, 1024
+    r, cam, sp = make("cornell", W, H, gpu)
+    sid, vlp = schedule(npass)
+    r.path_passes(sid, vlp)
+    col, _ = r.read_radiance()
+    lp = oracle.light_pass(sp, rnd0, 0)
+    ocol, _, _ = oracle.path_passes(sp, rnd0, cam, W, H, lp, sid, vlp)
+    linf = float(np.abs(col - ocol).max())
+    assert linf < 1e-3, linf
+    assert np.array_equal(col, ocol)           # and in practice bit-exact
+    r.close()
+
+
+def test_update_pixels_after_external_reduce(gpu):
+    r, _, _ = make("caustic", 20, 12, gpu)
+    sid, vlp = schedule(2)
+    r.path_passes(sid, vlp)
+    px = r.read_pixels()
+    r.update_pixels()
+    assert_same(r.read_pixels(), px, "pixels recomputed")
+    r.close()
+
+
+def test_smallpt_mirror_and_host_program(gpu, tmp_path):
+    """SmallPT (the Python mirror) and the C host program `smallpt` produce the same image."""
+    spt = g.SmallPT(32, 24, os.path.join(SCENES, "cornell.scn"), device=gpu)
+    spt.IdleFunc(1)                  # light pass + first path pass
+    spt.IdleFunc(3)
+    ppm_py = spt.SavePPM(str(tmp_path / "py.ppm"))
+    exe = os.path.join(REPO, "gpu_bidirectional_raytracer_amd", "smallpt")
+    out = tmp_path / "c.ppm"
+    subprocess.check_call([exe, "32", "24", os.path.join(SCENES, "cornell.scn"), "--spp", "4",
+                           "--batch", "1", "--out", str(out), "--dat",
+                           os.path.join(REPO, "assets", "data", "MersenneTwister.dat")], cwd=tmp_path)
+    assert open(ppm_py).read() == out.read_text()
+    spt.FreeBuffers()

@@ -1,0 +1,109 @@
+"""The CPU oracle against the reference's known answers and the committed
+fixtures.  No GPU needed."""
+import ctypes
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from conftest import GOLDEN, SCENES
+
+KA = json.load(open(os.path.join(GOLDEN, "known_answers.json")))
+
+
+@pytest.fixture(scope="module")
+def rnd0():
+    return oracle.mt607(0)
+
+
+def test_mt607_known_values(rnd0):
+    """d_Rand values recorded from RandomGPU (MersenneTwister_kernel.cu:63-110), seed 0."""
+    assert rnd0.shape == (KA["rand_n"],)
+    for k, v in KA["d_rand_seed0"].items():
+        assert rnd0[int(k)] == np.float32(v), (k, rnd0[int(k)], v)
+
+
+def test_mt607_range_and_seed_dependence(rnd0):
+    assert rnd0.min() > 0.0 and rnd0.max() <= 1.0            # ((float)x + 1) / 2^32 -> (0, 1]
+    rnd5 = oracle.mt607(5)
+    assert not np.array_equal(rnd0, rnd5)
+    # lanes are independent twisters: lane 0 of seed 0 differs from lane 1
+    assert not np.array_equal(rnd0[0::4096][:100], rnd0[1::4096][:100])
+    assert abs(float(rnd0.mean()) - 0.5) < 1e-3
+
+
+def test_mt607_matches_fixture(rnd0):
+    g = np.load(os.path.join(GOLDEN, "mt607.npz"))
+    np.testing.assert_array_equal(rnd0[g["idx"]], g["seed0"])
+    assert oracle.fnv1a64(rnd0) == int(g["fnv_seed0"])
+    assert oracle.fnv1a64(oracle.mt607(5)) == int(g["fnv_seed5"])
+
+
+def test_glibc_sid_sequence():
+    """sid = rand() % RAND_N, rand never seeded (smallpt_cpu.c:270)."""
+    libc = ctypes.CDLL("libc.so.6")
+    libc.srand(1)
+    sids = [libc.rand() % KA["rand_n"] for _ in range(5)]
+    assert sids == KA["sid_first5"]
+
+
+def test_cornell_vlp_known_answer(rnd0):
+    """dev_lp[1] of the cornell light pass (RadianceLightTracingKernel device.cu:222-455)."""
+    from make_golden import read_scene_py
+    _, _, sp = read_scene_py(os.path.join(SCENES, "cornell.scn"))
+    lp = oracle.light_pass(sp, rnd0, 0)
+    np.testing.assert_allclose(lp[1]["hp"], KA["cornell_dev_lp1"]["hp"], rtol=0, atol=6e-5)
+    np.testing.assert_array_equal(lp[1]["rad"], np.float32(KA["cornell_dev_lp1"]["rad"]))
+
+
+@pytest.mark.parametrize("name", json.load(open(os.path.join(GOLDEN, "render_meta.json")))["scenes"])
+def test_oracle_render_matches_fixture(rnd0, name):
+    from make_golden import read_scene_py
+    meta = json.load(open(os.path.join(GOLDEN, "render_meta.json")))
+    W, H = meta["internal_size"]
+    g = np.load(os.path.join(GOLDEN, f"render_{name}.npz"))
+    orig, target, sp = read_scene_py(os.path.join(SCENES, name + ".scn"))
+    cam = oracle.update_camera(orig, target, W, H)
+    np.testing.assert_array_equal(cam.view(np.float32).reshape(-1), g["camera"])
+    lp = oracle.light_pass(sp, rnd0, 0)
+    np.testing.assert_array_equal(lp.view(np.float32).reshape(-1, 9), g["lp"])
+    col, cnt, px = oracle.path_passes(sp, rnd0, cam, W, H, lp, meta["sid"], meta["vlp"])
+    np.testing.assert_array_equal(col, g["colors"])
+    np.testing.assert_array_equal(cnt, g["counter"])
+    np.testing.assert_array_equal(px, g["pixels"])
+    assert (cnt == meta["npass"]).all()
+
+
+def test_oracle_rows_partition_is_exact(rnd0):
+    """Rendering row bands separately and summing equals the full frame (fake multi-GPU)."""
+    from make_golden import read_scene_py
+    orig, target, sp = read_scene_py(os.path.join(SCENES, "cornell.scn"))
+    W, H = 41, 23
+    cam = oracle.update_camera(orig, target, W, H)
+    lp = oracle.light_pass(sp, rnd0, 0)
+    sid, vlp = [11, 222, 3333], [1, 1, 2]
+    full = oracle.path_passes(sp, rnd0, cam, W, H, lp, sid, vlp)
+    acc = [np.zeros_like(a) for a in full]
+    for y0 in range(0, H, 8):
+        part = oracle.path_passes(sp, rnd0, cam, W, H, lp, sid, vlp, rows=(y0, min(H, y0 + 8)))
+        for a, b in zip(acc, part):
+            a += b
+    for a, b in zip(acc, full):
+        np.testing.assert_array_equal(a, b)
+
+
+def test_oracle_counter_cap():
+    """counter[i] < 30000 (device.cu:607): no pass is added past the cap."""
+    from make_golden import read_scene_py
+    orig, target, sp = read_scene_py(os.path.join(SCENES, "simple.scn"))
+    W, H = 3, 2
+    rnd = oracle.mt607(0)
+    cam = oracle.update_camera(orig, target, W, H)
+    lp = oracle.light_pass(sp, rnd, 0)
+    cnt0 = np.full((H, W), 29998, np.uint32)
+    col0 = np.full((H, W, 3), 0.5, np.float32)
+    col, cnt, _ = oracle.path_passes(sp, rnd, cam, W, H, lp, [1, 2, 3, 4], [1, 1, 2, 2],
+                                     colors=col0, counter=cnt0)
+    assert (cnt == 30000).all()
