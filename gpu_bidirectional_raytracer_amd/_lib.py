@@ -100,7 +100,22 @@ _SIGS = [
 EXPORTED = [s[0] for s in _SIGS]
 
 
+def _single_hip_runtime():
+    """Exactly one HIP runtime per process.  torch bundles its own libamdhip64/libhsa-runtime64
+    (same SONAME libamdhip64.so.7 as /opt/rocm's).  If libbdpt.so loaded the system runtime first,
+    a later `import torch` would map a second HSA runtime that cannot open the device.  Loading
+    torch first makes libbdpt.so bind to torch's runtime, so device pointers can be shared with
+    torch.distributed (RCCL) in the same process.  Without torch the system runtime is used."""
+    if os.environ.get("BDPT_NO_TORCH") == "1":
+        return
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def _load():
+    _single_hip_runtime()
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"{LIB_PATH} is not built: run `make` (or __graft_entry__.build()) first; "
                           "there is no CPU fallback for the render path")

@@ -1,0 +1,30 @@
+#!/bin/bash
+# One GPU-box session: parity tests, bench, rocprofv3 kernel trace.  Each GPU step has its own
+# time limit; a crash/abort/timeout (exit >= 124 or signal) stops the script.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+ok_or_stop() {  # $1 = exit code, $2 = step name; test failures (1) continue, faults stop
+  if [ "$1" -ne 0 ] && [ "$1" -ne 1 ]; then echo "STOP after $2 (exit $1)"; exit "$1"; fi
+}
+STEPS="${STEPS:-tests bench prof}"
+for s in $STEPS; do
+  case "$s" in
+  tests)
+    timeout -k 10 600 python -m pytest tests -m gpu -q -rA > gpurun_out/pytest_gpu.log 2>&1
+    rc=$?; tail -30 gpurun_out/pytest_gpu.log; ok_or_stop $rc tests ;;
+  smoke)
+    timeout -k 10 300 python -c "import __graft_entry__ as e; e.smoke()" > gpurun_out/smoke.log 2>&1
+    rc=$?; cat gpurun_out/smoke.log; ok_or_stop $rc smoke ;;
+  bench)
+    timeout -k 10 400 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1
+    rc=$?; tail -5 gpurun_out/bench.log; ok_or_stop $rc bench ;;
+  prof)
+    rm -rf gpurun_out/prof
+    timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
+        python3 bench.py --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/prof.log 2>&1
+    rc=$?; tail -3 gpurun_out/prof.log; find gpurun_out/prof -name "*stats*" | head; ok_or_stop $rc prof ;;
+  esac
+done
+echo ALL_DONE
