@@ -34,6 +34,9 @@ struct bdpt_path_args {
     unsigned n;
     unsigned n_lights;
     const int* lights;              // indices of emitters (e != 0), ascending
+    const float4* lightrec;         // per emitter: {p, rad}, {e, (4*pi*rad)*rad}
+    const float4* geom;             // per sphere {p, rad*rad} (SGPR-resident traversal)
+    unsigned emis_mask;             // bit s = sphere s is emissive (sphere counts <= 32)
     const float* rnd;
     const bdpt_dev_lightpath* lp;
     const unsigned* sid;            // per pass

@@ -27,7 +27,7 @@ static_assert(sizeof(bdpt_dev_vec) == sizeof(bdpt_vec), "colour layout");
 extern "C" __global__ void bdpt_mt607_kernel(const uint4*, unsigned, float*);
 extern "C" __global__ void bdpt_light_kernel(const bdpt_dev_sphere*, unsigned, const float*, int,
                                              bdpt_dev_lightpath*);
-extern "C" __global__ void bdpt_path_kernel(bdpt_path_args);
+extern "C" const void* bdpt_path_kernel_table[17];   // [n] for n <= 16, [0] generic
 extern "C" __global__ void bdpt_pixels_kernel(const bdpt_dev_vec*, uchar4*, const float*, int);
 
 // gamma thresholds (host, once): see bdpt_util.c
@@ -55,6 +55,9 @@ struct bdpt_ctx {
     bdpt_dev_sphere* d_sph = nullptr;
     unsigned sph_cap = 0;
     int* d_lights = nullptr;
+    float4* d_geom = nullptr;           // per sphere {p, rad^2}
+    float4* d_lightrec = nullptr;       // per emitter {p, rad}, {e, (4*pi*rad)*rad}
+    unsigned emis_mask = 0;
     bdpt_dev_vec* d_colors = nullptr;
     unsigned* d_counter = nullptr;
     uchar4* d_pixels = nullptr;
@@ -86,7 +89,9 @@ static int fail(bdpt_ctx* c, int code, const char* fmt, ...) {
 static int upload_scene(bdpt_ctx* c) {
     const unsigned n = (unsigned)c->spheres.size();
     std::vector<bdpt_dev_sphere> ds(n);
+    std::vector<float4> geom(n), lrec;
     c->lights.clear();
+    c->emis_mask = 0;
     for (unsigned i = 0; i < n; i++) {
         const bdpt_sphere& s = c->spheres[i];
         bdpt_dev_sphere& d = ds[i];
@@ -96,16 +101,31 @@ static int upload_scene(bdpt_ctx* c) {
         d.rad = s.rad;
         d.cx = s.c.x; d.cy = s.c.y; d.cz = s.c.z;
         d.refl = s.refl;
-        if (!(s.e.x == 0.f && s.e.y == 0.f && s.e.z == 0.f)) c->lights.push_back((int)i);
+        geom[i] = make_float4(d.px, d.py, d.pz, d.rr);
+        if (!(s.e.x == 0.f && s.e.y == 0.f && s.e.z == 0.f)) {
+            c->lights.push_back((int)i);
+            if (i < 32) c->emis_mask |= 1u << i;
+            const float kPi = 3.14159265358979323846f;
+            const float area = 4.f * kPi * s.rad * s.rad;        // device.cu:500, same float ops
+            lrec.push_back(make_float4(s.p.x, s.p.y, s.p.z, s.rad));
+            lrec.push_back(make_float4(s.e.x, s.e.y, s.e.z, area));
+        }
     }
     if (n > c->sph_cap) {
-        if (c->d_sph) HIPCHK(c, hipFree(c->d_sph));
-        if (c->d_lights) HIPCHK(c, hipFree(c->d_lights));
-        c->d_sph = nullptr; c->d_lights = nullptr;
+        void* old[] = {c->d_sph, c->d_lights, c->d_geom, c->d_lightrec};
+        for (void* b : old)
+            if (b) HIPCHK(c, hipFree(b));
+        c->d_sph = nullptr; c->d_lights = nullptr; c->d_geom = nullptr; c->d_lightrec = nullptr;
         HIPCHK(c, hipMalloc(&c->d_sph, sizeof(bdpt_dev_sphere) * n));
         HIPCHK(c, hipMalloc(&c->d_lights, sizeof(int) * n));
+        HIPCHK(c, hipMalloc(&c->d_geom, sizeof(float4) * n));
+        HIPCHK(c, hipMalloc(&c->d_lightrec, 2 * sizeof(float4) * n));
         c->sph_cap = n;
     }
+    if (n) HIPCHK(c, hipMemcpyAsync(c->d_geom, geom.data(), sizeof(float4) * n, hipMemcpyHostToDevice, c->stream));
+    if (!lrec.empty())
+        HIPCHK(c, hipMemcpyAsync(c->d_lightrec, lrec.data(), sizeof(float4) * lrec.size(),
+                                 hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemcpyAsync(c->d_sph, ds.data(), sizeof(bdpt_dev_sphere) * n, hipMemcpyHostToDevice, c->stream));
     if (!c->lights.empty())
         HIPCHK(c, hipMemcpyAsync(c->d_lights, c->lights.data(), sizeof(int) * c->lights.size(),
@@ -115,7 +135,7 @@ static int upload_scene(bdpt_ctx* c) {
 }
 
 static void release(bdpt_ctx* c) {
-    void* bufs[] = {c->d_params, c->d_rand, c->d_lp, c->d_sph, c->d_lights, c->d_colors,
+    void* bufs[] = {c->d_params, c->d_rand, c->d_lp, c->d_sph, c->d_lights, c->d_geom, c->d_lightrec, c->d_colors,
                     c->d_counter, c->d_pixels, c->d_thr, c->d_sid, c->d_vlp};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -299,6 +319,9 @@ int bdpt_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int npass
     a.n = (unsigned)c->spheres.size();
     a.n_lights = (unsigned)c->lights.size();
     a.lights = c->d_lights;
+    a.lightrec = c->d_lightrec;
+    a.geom = c->d_geom;
+    a.emis_mask = c->emis_mask;
     a.rnd = c->d_rand;
     a.lp = c->d_lp;
     a.colors = c->d_colors;
@@ -326,19 +349,23 @@ int bdpt_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int npass
     a.shard = c->shard; a.nshards = c->nshards; a.band_rows = c->band_rows;
 
     dim3 grid((c->W + 15) / 16, (c->H + 15) / 16), block(256);
-    const size_t smem = sizeof(float4) * 4 * (a.n ? a.n : 1);
-    // keep single launches bounded (~2^28 samples) so no dispatch runs for many seconds
+    const void* kern = bdpt_path_kernel_table[a.n <= 16 ? a.n : 0];
+    // keep single launches bounded (~2^28 samples, <= 256 passes for the LDS pass tables)
     const long per_pass = (long)c->W * c->H;
     int chunk = (int)((1L << 28) / (per_pass > 0 ? per_pass : 1));
     if (chunk < 1) chunk = 1;
+    if (chunk > 256) chunk = 256;
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     int launches = 0;
     for (int p0 = 0; p0 < npass; p0 += chunk, launches++) {
         a.sid = c->d_sid + p0;
         a.vlp = c->d_vlp + p0;
         a.npass = npass - p0 < chunk ? npass - p0 : chunk;
-        hipLaunchKernelGGL(bdpt_path_kernel, grid, block, smem, c->stream, a);
-        HIPCHK(c, hipGetLastError());
+        const size_t smem = sizeof(float4) * (4 * (size_t)a.n + 3 * (size_t)a.npass) + sizeof(unsigned) * a.npass;
+        if (smem > 160 * 1024)
+            return fail(c, BDPT_EINVAL, "bdpt_path_passes: scene too large for LDS (%u spheres)", a.n);
+        void* kargs[] = {&a};
+        HIPCHK(c, hipLaunchKernel(kern, grid, block, kargs, smem, c->stream));
     }
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
     c->timed = true;

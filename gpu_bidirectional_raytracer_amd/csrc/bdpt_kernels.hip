@@ -11,6 +11,7 @@
 #include <stdint.h>
 #include <utility>
 #include "bdpt_device.h"
+#include "bdpt_math.h"
 
 namespace {
 
@@ -23,7 +24,7 @@ __device__ __forceinline__ f3 sub(f3 a, f3 b) { return mk(a.x - b.x, a.y - b.y, 
 __device__ __forceinline__ f3 mul(f3 a, f3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
 __device__ __forceinline__ f3 smul(float k, f3 b) { return mk(k * b.x, k * b.y, k * b.z); }
 __device__ __forceinline__ float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
-__device__ __forceinline__ f3 norm(f3 v) { float l = 1.f / sqrtf(dot(v, v)); return smul(l, v); }
+__device__ __forceinline__ f3 norm(f3 v) { float l = 1.f / bdpt_sqrt_rn(dot(v, v)); return smul(l, v); }
 __device__ __forceinline__ f3 cross(f3 a, f3 b) {
     return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }
@@ -33,10 +34,10 @@ constexpr float kEps = 0.01f;                              // geom.h:6 EPSILON
 constexpr float kPi = 3.14159265358979323846f;             // geom.h:7 FLOAT_PI
 constexpr unsigned kRandN = BDPT_DEV_RAND_N;
 
-// sinf/cosf with correctly-rounded semantics: fp64 sincos rounded once to fp32.
+// sinf/cosf with correctly-rounded semantics: fp64 sincos rounded once to fp32 (bdpt_math.h).
 __device__ __forceinline__ void sincos_cr(float x, float* s, float* c) {
     double sd, cd;
-    sincos((double)x, &sd, &cd);
+    bdpt_sincos_dp((double)x, &sd, &cd);
     *s = (float)sd;
     *c = (float)cd;
 }
@@ -47,7 +48,7 @@ __device__ __forceinline__ float sphere_isect(float4 g, f3 o, f3 d) {
     float b = dot(op, d);
     float det = b * b - dot(op, op) + g.w;
     if (det < 0.f) return 0.f;
-    det = sqrtf(det);
+    det = bdpt_sqrt_rn(det);
     float t = b - det;
     if (t > kEps) return t;
     t = b + det;
@@ -58,7 +59,7 @@ __device__ __forceinline__ float sphere_isect(float4 g, f3 o, f3 d) {
 __device__ __forceinline__ f3 uniform_sphere(float u1, float u2) {
     const float zz = 1.f - 2.f * u1;
     const float q = 1.f - zz * zz;
-    const float r = sqrtf(0.f > q ? 0.f : q);
+    const float r = bdpt_sqrt_rn(0.f > q ? 0.f : q);
     const float phi = 2.f * kPi * u2;
     float s, c;
     sincos_cr(phi, &s, &c);
@@ -69,7 +70,7 @@ __device__ __forceinline__ f3 uniform_sphere(float u1, float u2) {
 __device__ __forceinline__ f3 cosine_dir(f3 w, float u_phi, float u_r2) {
     const float r1 = 2.f * kPi * u_phi;
     const float r2 = u_r2;
-    const float r2s = sqrtf(r2);
+    const float r2s = bdpt_sqrt_rn(r2);
     f3 a = fabsf(w.x) > .1f ? mk(0.f, 1.f, 0.f) : mk(1.f, 0.f, 0.f);
     f3 u = norm(cross(a, w));
     f3 v = cross(w, u);
@@ -78,7 +79,7 @@ __device__ __forceinline__ f3 cosine_dir(f3 w, float u_phi, float u_r2) {
     u = smul(c * r2s, u);
     v = smul(s * r2s, v);
     f3 nd = add(u, v);
-    w = smul(sqrtf(1 - r2), w);
+    w = smul(bdpt_sqrt_rn(1 - r2), w);
     return add(nd, w);
 }
 
@@ -191,28 +192,67 @@ extern "C" __global__ __launch_bounds__(64) void bdpt_light_kernel(const bdpt_de
 //  * One lane = one pixel for the whole launch; the running mean (c*k1 + r)*k2 and the counter
 //    stay in VGPRs across passes and are written once, coalesced, at the end (36 B/pixel/launch).
 //  * Path regeneration: one loop iteration = one path segment for every live lane; a lane whose
-//    path ends accumulates and immediately starts its next pass, so lanes never idle waiting for
-//    the longest path of the wave (the reference's 1-spp launch idles them).
-//  * The sphere list is staged in LDS once per workgroup ({p, rad^2} for traversal, emission /
-//    colour / material for shading); traversal reads are wave-uniform broadcasts.
+//    path ends accumulates and starts its next pass in the next iteration, so lanes never idle
+//    waiting for the longest path of the wave (the reference's 1-spp launch idles them).
+//  * Sphere geometry {p, rad^2}: for N = 1..16 spheres (template) it is loaded once into SGPRs and
+//    every traversal loop is fully unrolled; otherwise (N = 0) it is staged in LDS and read as a
+//    wave-uniform broadcast.  Emission / colour / material / centre for the per-lane hit id are
+//    LDS tables; the per-pass sid and VLP (the reference's dev_lp[vlp_index]) are LDS tables too.
+//  * The 5 random numbers a segment may consume (d_Rand[j..j+4], j = (26+25i+5*depth+sid) mod
+//    (RAND_N-5), device.cu:619) are prefetched one segment ahead, so the L2/MALL gather latency
+//    hides behind the traversal of the current segment.
 //  * 256-thread workgroup = 16x16 pixel tile as 2x2 waves of 8x8 pixels (2-D tiles keep the
 //    paths of a wave coherent).
 // =============================================================================================
-extern "C" __global__ __launch_bounds__(256) void bdpt_path_kernel(bdpt_path_args a) {
+template <int N>
+__global__ __launch_bounds__(256) void bdpt_path_kernel_t(bdpt_path_args a) {
     extern __shared__ float4 smem[];
-    float4* G = smem;                 // {px, py, pz, rad*rad}
-    float4* E = smem + a.n;           // {ex, ey, ez, rad}
-    float4* C = smem + 2 * a.n;       // {cx, cy, cz, bits(refl | emissive<<8)}
-    float4* P = smem + 3 * a.n;       // {px, py, pz, 0} (hit normal)
-    for (unsigned s = threadIdx.x; s < a.n; s += 256) {
+    const int n = N > 0 ? N : (int)a.n;
+    constexpr int kUnroll = N > 0 ? N : 1;
+    float4* C = smem;                 // {cx, cy, cz, bits(refl | emissive<<8)}
+    float4* E = smem + n;             // {ex, ey, ez, rad}
+    float4* P = smem + 2 * n;         // {px, py, pz, 0}  (hit normal)
+    float4* G = smem + 3 * n;         // {px, py, pz, rad^2}  (N == 0 traversal)
+    float4* V = smem + 4 * n;         // per pass: VLP {hx,hy,hz,rx}{ry,rz,nx,ny}{nz,-,-,-}
+    unsigned* SID = (unsigned*)(V + 3 * a.npass);
+    for (int s = threadIdx.x; s < n; s += 256) {
         const bdpt_dev_sphere S = a.sph[s];
-        G[s] = make_float4(S.px, S.py, S.pz, S.rr);
-        E[s] = make_float4(S.ex, S.ey, S.ez, S.rad);
         const bool emis = !(S.ex == 0.f && S.ey == 0.f && S.ez == 0.f);
         C[s] = make_float4(S.cx, S.cy, S.cz, __int_as_float(S.refl | (emis ? 256 : 0)));
+        E[s] = make_float4(S.ex, S.ey, S.ez, S.rad);
         P[s] = make_float4(S.px, S.py, S.pz, 0.f);
+        G[s] = make_float4(S.px, S.py, S.pz, S.rr);
+    }
+    for (int q = threadIdx.x; q < a.npass; q += 256) {
+        const bdpt_dev_lightpath L = a.lp[a.vlp[q] & (BDPT_DEV_LIGHT_POINTS - 1)];
+        V[3 * q + 0] = make_float4(L.hx, L.hy, L.hz, L.rx);
+        V[3 * q + 1] = make_float4(L.ry, L.rz, L.nx, L.ny);
+        V[3 * q + 2] = make_float4(L.nz, 0.f, 0.f, 0.f);
+        SID[q] = a.sid[q];
     }
     __syncthreads();
+
+    float4 g[N > 0 ? N : 1];
+    if constexpr (N > 0) {
+#pragma unroll
+        for (int s = 0; s < N; s++) g[s] = a.geom[s];           // wave-uniform: SGPRs
+    }
+    auto geom = [&](int s) -> float4 {
+        if constexpr (N > 0) return g[s]; else return G[s];
+    };
+    auto emissive = [&](int s) -> bool {
+        if constexpr (N > 0) return (a.emis_mask >> s) & 1u;
+        else return (__float_as_int(C[s].w) & 256) != 0;
+    };
+    // IntersectPDevice / IntersectPVacuumDevice (device.cu:126-154): any hit in (0, maxt)
+    auto occluded = [&](f3 o, f3 d, float maxt, bool vacuum) -> bool {
+#pragma unroll kUnroll
+        for (int s = n - 1; s >= 0; --s) {
+            const float dd = sphere_isect(geom(s), o, d);
+            if (dd != 0.f && dd < maxt && !(vacuum && emissive(s))) return true;
+        }
+        return false;
+    };
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
@@ -224,34 +264,31 @@ extern "C" __global__ __launch_bounds__(256) void bdpt_path_kernel(bdpt_path_arg
     const int i = y * a.W + x;
     const unsigned ibase = 26u + (unsigned)(i * 25);
     const float* __restrict__ rnd = a.rnd;
+    constexpr unsigned M5 = kRandN - 5u;
 
-    // running mean state (device.cu:774-787)
     bdpt_dev_vec cv = a.colors[i];
     f3 col = mk(cv.x, cv.y, cv.z);
     unsigned cnt = a.counter[i];
     const unsigned cnt0 = cnt;
 
-    // camera constants (device.cu:562-600), computed on the host with the same float ops
     const f3 ux = mk(a.ux[0], a.ux[1], a.ux[2]);
     const f3 uy = mk(a.uy[0], a.uy[1], a.uy[2]);
     const f3 ud = mk(a.ud[0], a.ud[1], a.ud[2]);
     const f3 org = mk(a.orig[0], a.orig[1], a.orig[2]);
-    const double kx0 = (double)((float)x * a.inv_w) - a.half_w;
+    const double kx0 = (double)((float)x * a.inv_w) - a.half_w;   // device.cu:565-566
     const double ky0 = (double)((float)y * a.inv_h) - a.half_h;
 
     int p = 0;
+    unsigned depth = 0, sid = SID[0];
+    unsigned j = (ibase + sid) % M5;
+    float q0 = rnd[j], q1 = rnd[j + 1], q2 = rnd[j + 2], q3 = rnd[j + 3], q4 = rnd[j + 4];
     f3 ro = mk(0.f, 0.f, 0.f), rd = ro, thr = ro, rad = ro;
-    unsigned depth = 0, sid = 0;
-    int vlp = 0;
     bool specular = true, fresh = true;
 
     while (p < a.npass && cnt < BDPT_DEV_COUNTER_CAP) {
-        if (fresh) {                                                     // camera ray (:562-600)
-            sid = a.sid[p];
-            vlp = a.vlp[p] & (BDPT_DEV_LIGHT_POINTS - 1);
-            const unsigned kk = (ibase + sid) % (kRandN - 5u);
-            const float kx = (float)(kx0 + (double)(rnd[kk] * a.inv_w));
-            const float ky = (float)(ky0 + (double)(rnd[kk + 1] * a.inv_h));
+        if (fresh) {                          // camera ray (:562-600); d_Rand[kk] == q0 (kk == j)
+            const float kx = (float)(kx0 + (double)(q0 * a.inv_w));
+            const float ky = (float)(ky0 + (double)(q1 * a.inv_h));
             const float kz = 10.0f;
             f3 rdir = mk(0.f, 0.f, 0.f);
             rdir = add(rdir, smul(kx, ux));
@@ -264,16 +301,15 @@ extern "C" __global__ __launch_bounds__(256) void bdpt_path_kernel(bdpt_path_arg
             rad = mk(0.f, 0.f, 0.f);
             thr = mk(1.f, 1.f, 1.f);
             specular = true;
-            depth = 0;
             fresh = false;
         }
-        const unsigned j = (ibase + depth * 5u + sid) % (kRandN - 5u);
 
         // closest hit, scanning from the last sphere down (device.cu:106-124)
         float t = 1e20f;
         int id = -1;
-        for (int s = (int)a.n - 1; s >= 0; --s) {
-            const float d = sphere_isect(G[s], ro, rd);
+#pragma unroll kUnroll
+        for (int s = n - 1; s >= 0; --s) {
+            const float d = sphere_isect(geom(s), ro, rd);
             if (d != 0.f && d < t) { t = d; id = s; }
         }
         bool done = id < 0;
@@ -294,57 +330,39 @@ extern "C" __global__ __launch_bounds__(256) void bdpt_path_kernel(bdpt_path_arg
             } else if ((mat & 255) == BDPT_DEV_DIFF) {                   // :663-703
                 specular = false;
                 thr = mul(thr, mk(cm.x, cm.y, cm.z));
-                // SampleLightsDevice(.., nn = j+2) device.cu:457-542
+                // SampleLightsDevice(.., nn = j+2) device.cu:457-542: d_Rand[j+3], d_Rand[j+4]
                 f3 res = mk(0.f, 0.f, 0.f);
-                const unsigned dk = j + 3, dj = j + 4;
-                for (unsigned li = 0; li < a.n_lights; li++) {
-                    const int ls = a.lights[li];
-                    const float4 le = E[ls];
-                    const float4 lg = G[ls];
-                    const f3 usp = uniform_sphere(rnd[dk], rnd[dj]);
-                    const f3 spt = add(smul(le.w, usp), mk(lg.x, lg.y, lg.z));
-                    f3 sd = sub(spt, hit);
-                    const float len = sqrtf(dot(sd, sd));
-                    sd = smul(1.f / len, sd);
-                    float wo = dot(sd, usp);
-                    if (wo > 0.f) continue;
-                    wo = -wo;
-                    const float wi = dot(sd, nl);
-                    if (wi > 0.f) {
-                        const float maxt = len - kEps;
-                        bool occluded = false;
-                        for (int s = (int)a.n - 1; s >= 0; --s) {
-                            const float d = sphere_isect(G[s], hit, sd);
-                            if (d != 0.f && d < maxt) { occluded = true; break; }
-                        }
-                        if (!occluded) {
-                            const float sc = (4.f * kPi * le.w * le.w) * wi * wo / (len * len);
+                if (a.n_lights) {
+                    const f3 usp = uniform_sphere(q3, q4);               // same for every light
+                    for (unsigned li = 0; li < a.n_lights; li++) {
+                        const float4 lg = a.lightrec[2 * li];             // {p, rad}
+                        const float4 le = a.lightrec[2 * li + 1];         // {e, 4*pi*rad*rad}
+                        const f3 spt = add(smul(lg.w, usp), mk(lg.x, lg.y, lg.z));
+                        f3 sd = sub(spt, hit);
+                        const float len = bdpt_sqrt_rn(dot(sd, sd));
+                        sd = smul(1.f / len, sd);
+                        float wo = dot(sd, usp);
+                        if (wo > 0.f) continue;
+                        wo = -wo;
+                        const float wi = dot(sd, nl);
+                        if (wi > 0.f && !occluded(hit, sd, len - kEps, false)) {
+                            const float sc = le.w * wi * wo / (len * len);
                             res = add(res, smul(sc, mk(le.x, le.y, le.z)));
                         }
                     }
                 }
                 f3 vres = mk(0.f, 0.f, 0.f);
                 {
-                    const bdpt_dev_lightpath L = a.lp[vlp];
-                    f3 sd = sub(mk(L.hx, L.hy, L.hz), hit);
-                    const float len = sqrtf(dot(sd, sd));
+                    const float4 v0 = V[3 * p], v1 = V[3 * p + 1], v2 = V[3 * p + 2];
+                    f3 sd = sub(mk(v0.x, v0.y, v0.z), hit);
+                    const float len = bdpt_sqrt_rn(dot(sd, sd));
                     sd = smul(1.f / len, sd);
-                    float wo = dot(sd, mk(L.nx, L.ny, L.nz));
+                    float wo = dot(sd, mk(v1.z, v1.w, v2.x));
                     if (!(wo > 0.f)) {
                         wo = -wo;
                         const float wi = dot(sd, nl);
-                        if (wi > 0.f) {
-                            const float maxt = len - kEps;
-                            bool occluded = false;
-                            for (int s = (int)a.n - 1; s >= 0; --s) {
-                                const float d = sphere_isect(G[s], hit, sd);
-                                if (d != 0.f && d < maxt && !(__float_as_int(C[s].w) & 256)) {
-                                    occluded = true;
-                                    break;
-                                }
-                            }
-                            if (!occluded) vres = add(vres, smul(wi * wo, mk(L.rx, L.ry, L.rz)));
-                        }
+                        if (wi > 0.f && !occluded(hit, sd, len - kEps, true))
+                            vres = add(vres, smul(wi * wo, mk(v0.w, v1.x, v1.y)));
                     }
                 }
                 vres = smul(1.f, vres);
@@ -352,7 +370,7 @@ extern "C" __global__ __launch_bounds__(256) void bdpt_path_kernel(bdpt_path_arg
                 res = smul(0.5f, res);
                 rad = add(rad, mul(res, thr));
                 ro = hit;
-                rd = cosine_dir(nl, rnd[j], rnd[j + 1]);
+                rd = cosine_dir(nl, q0, q1);
             } else if ((mat & 255) == BDPT_DEV_SPEC) {                   // :704-714
                 specular = true;
                 const f3 nd = sub(rd, smul(2.f * dot(normal, rd), normal));
@@ -372,17 +390,17 @@ extern "C" __global__ __launch_bounds__(256) void bdpt_path_kernel(bdpt_path_arg
                     ro = hit;
                     rd = refl;
                 } else {
-                    const float kq = (float)(into ? 1 : -1) * (ddn * nnt + sqrtf(cos2t));
+                    const float kq = (float)(into ? 1 : -1) * (ddn * nnt + bdpt_sqrt_rn(cos2t));
                     const f3 td = norm(sub(smul(nnt, rd), smul(kq, normal)));
                     const float aa = nt - nc, bb = nt + nc;
                     const float R0 = aa * aa / (bb * bb);
                     const float c = 1 - (into ? -ddn : dot(td, normal));
                     const float Re = R0 + (1 - R0) * c * c * c * c * c;
                     const float Tr = 1.f - Re;
-                    const float P = .25f + .5f * Re;
-                    const float RP = Re / P;
-                    const float TP = Tr / (1.f - P);
-                    if (rnd[j + 2] < P) {
+                    const float Pp = .25f + .5f * Re;
+                    const float RP = Re / Pp;
+                    const float TP = Tr / (1.f - Pp);
+                    if (q2 < Pp) {
                         thr = mul(smul(RP, thr), mk(cm.x, cm.y, cm.z));
                         rd = refl;
                     } else {
@@ -407,7 +425,12 @@ extern "C" __global__ __launch_bounds__(256) void bdpt_path_kernel(bdpt_path_arg
             cnt++;
             p++;
             fresh = true;
+            depth = 0;
+            if (p < a.npass) sid = SID[p];
         }
+        // prefetch the random numbers of the next segment (device.cu:619)
+        j = (ibase + depth * 5u + sid) % M5;
+        q0 = rnd[j]; q1 = rnd[j + 1]; q2 = rnd[j + 2]; q3 = rnd[j + 3]; q4 = rnd[j + 4];
     }
     if (cnt == cnt0) return;                                             // nothing rendered
     bdpt_dev_vec out;
@@ -416,6 +439,24 @@ extern "C" __global__ __launch_bounds__(256) void bdpt_path_kernel(bdpt_path_arg
     a.counter[i] = cnt;
     a.pixels[i] = bdpt_dev_to_rgba(col.x, col.y, col.z, a.gamma_thr);
 }
+
+#define BDPT_INST(NN) template __global__ void bdpt_path_kernel_t<NN>(bdpt_path_args);
+BDPT_INST(0) BDPT_INST(1) BDPT_INST(2) BDPT_INST(3) BDPT_INST(4) BDPT_INST(5) BDPT_INST(6)
+BDPT_INST(7) BDPT_INST(8) BDPT_INST(9) BDPT_INST(10) BDPT_INST(11) BDPT_INST(12)
+BDPT_INST(13) BDPT_INST(14) BDPT_INST(15) BDPT_INST(16)
+#undef BDPT_INST
+
+// host-side launch table (index = sphere count, 0 = generic LDS traversal)
+extern "C" const void* bdpt_path_kernel_table[17] = {
+    (const void*)&bdpt_path_kernel_t<0>, (const void*)&bdpt_path_kernel_t<1>,
+    (const void*)&bdpt_path_kernel_t<2>, (const void*)&bdpt_path_kernel_t<3>,
+    (const void*)&bdpt_path_kernel_t<4>, (const void*)&bdpt_path_kernel_t<5>,
+    (const void*)&bdpt_path_kernel_t<6>, (const void*)&bdpt_path_kernel_t<7>,
+    (const void*)&bdpt_path_kernel_t<8>, (const void*)&bdpt_path_kernel_t<9>,
+    (const void*)&bdpt_path_kernel_t<10>, (const void*)&bdpt_path_kernel_t<11>,
+    (const void*)&bdpt_path_kernel_t<12>, (const void*)&bdpt_path_kernel_t<13>,
+    (const void*)&bdpt_path_kernel_t<14>, (const void*)&bdpt_path_kernel_t<15>,
+    (const void*)&bdpt_path_kernel_t<16>};
 
 // Recompute pixels from colors (after a cross-GPU reduce of the radiance frame).
 extern "C" __global__ __launch_bounds__(256) void bdpt_pixels_kernel(const bdpt_dev_vec* __restrict__ colors,

@@ -1,0 +1,60 @@
+// bdpt_math.h -- the transcendental / root functions of the render path with the exact results
+// the oracle's contract requires, cheaper than the generic library sequences.
+//
+//  * bdpt_sincos_dp: fp64 sin & cos (Cody-Waite reduction by pi/2 with a 33-bit head, fdlibm's
+//    degree-13/14 minimax kernels, explicit fma).  Only ever called on x = 2*pi*u with u an MT607
+//    float; tests/test_math.py sweeps every float such an x can take (2^28 of them) and checks that
+//    (float)result equals (float)sin((double)x) / (float)cos((double)x) of glibc for all of them.
+//    Host+device so the same code is what the test runs.
+//  * bdpt_sqrt_rn (device): correctly rounded fp32 sqrt = v_sqrt_f32 plus the +-1 ulp residual
+//    correction; inputs below 2^-96 (and 0, NaN, negatives) take the library sequence on an
+//    exec-masked branch, so the result equals sqrtf() for every input.
+#ifndef BDPT_MATH_H
+#define BDPT_MATH_H
+
+#include <math.h>
+
+#if defined(__HIPCC__)
+#define BDPT_HD __host__ __device__ __forceinline__
+#else
+#define BDPT_HD static inline
+#endif
+
+BDPT_HD void bdpt_sincos_dp(double x, double* so, double* co) {
+    const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
+                 S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
+                 S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
+    const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
+                 C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
+                 C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
+    const double P1 = 1.57079632673412561417e+00;   // pi/2, first 33 bits: k*P1 is exact
+    const double P1T = 6.07710050650619224932e-11;  // pi/2 - P1
+    const double k = rint(x * 0.63661977236758134308);
+    const int q = (int)k;
+    const double r = fma(-k, P1T, fma(-k, P1, x));  // x - k*P1 exact (Sterbenz), then the tail
+    const double z = r * r;
+    const double ps = fma(z, fma(z, fma(z, fma(z, fma(z, S6, S5), S4), S3), S2), S1);
+    const double s = fma(r * z, ps, r);
+    const double pc = fma(z, fma(z, fma(z, fma(z, fma(z, C6, C5), C4), C3), C2), C1);
+    const double hz = 0.5 * z, w = 1.0 - hz;
+    const double c = w + (((1.0 - w) - hz) + z * z * pc);
+    const double sn = (q & 1) ? c : s, cs = (q & 1) ? s : c;
+    *so = (q & 2) ? -sn : sn;
+    *co = ((q + 1) & 2) ? -cs : cs;
+}
+
+#if defined(__HIPCC__)
+__device__ __forceinline__ float bdpt_sqrt_rn(float x) {
+    if (__builtin_expect(!(x >= 0x1p-96f), 0)) return sqrtf(x);
+    float s = __builtin_amdgcn_sqrtf(x);
+    const float sdn = __int_as_float(__float_as_int(s) - 1);
+    const float sup = __int_as_float(__float_as_int(s) + 1);
+    const float rdn = __builtin_fmaf(-sdn, s, x);
+    const float rup = __builtin_fmaf(-sup, s, x);
+    s = rdn <= 0.f ? sdn : s;
+    s = rup > 0.f ? sup : s;
+    return s;
+}
+#endif
+
+#endif

@@ -9,6 +9,13 @@ ok_or_stop() {  # $1 = exit code, $2 = step name; test failures (1) continue, fa
   if [ "$1" -ne 0 ] && [ "$1" -ne 1 ]; then echo "STOP after $2 (exit $1)"; exit "$1"; fi
 }
 STEPS="${STEPS:-tests bench prof}"
+PMC_SETS=(
+  "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM GRBM_GUI_ACTIVE"
+  "SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT"
+  "FETCH_SIZE"
+  "WRITE_SIZE"
+  "TCC_HIT_sum TCC_MISS_sum"
+)
 for s in $STEPS; do
   case "$s" in
   tests)
@@ -25,6 +32,15 @@ for s in $STEPS; do
     timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
         python3 bench.py --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/prof.log 2>&1
     rc=$?; tail -3 gpurun_out/prof.log; find gpurun_out/prof -name "*stats*" | head; ok_or_stop $rc prof ;;
+  pmc)
+    rocprofv3 -L > gpurun_out/counters_list.txt 2>&1 || true
+    i=0
+    for set in "${PMC_SETS[@]}"; do
+      i=$((i+1)); rm -rf gpurun_out/pmc$i
+      timeout -k 10 300 rocprofv3 --pmc $set --kernel-trace -d gpurun_out/pmc$i -o run --output-format csv -- \
+          python3 bench.py --no-cpu-baseline --steps 4 --warmup 1 ${BENCH_ARGS:-} > gpurun_out/pmc$i.log 2>&1
+      rc=$?; echo "pmc set $i ($set): rc=$rc"; tail -2 gpurun_out/pmc$i.log; ok_or_stop $rc pmc$i
+    done ;;
   esac
 done
 echo ALL_DONE
