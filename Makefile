@@ -6,14 +6,15 @@
 
 PKG      := gpu_bidirectional_raytracer_amd
 CSRC     := $(PKG)/csrc
-BUILD    := $(PKG)/_build
+BUILD    ?= $(PKG)/_build
 HIPCC    ?= /opt/rocm/bin/hipcc
 ARCH     ?= gfx950
 CC       ?= gcc
-HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -fno-slp-vectorize \
+            -Wall -Wno-unused-function $(EXTRA_HIPFLAGS)
 CFLAGS   := -O2 -std=gnu11 -fPIC -ffp-contract=off -Wall -Wextra -Wno-unused-parameter
 
-LIB      := $(PKG)/libbdpt.so
+LIB      ?= $(PKG)/libbdpt.so
 HOST     := $(PKG)/smallpt
 ORACLE   := oracle/liboracle.so
 
@@ -22,7 +23,7 @@ all: $(LIB) $(HOST) $(ORACLE)
 $(BUILD):
 	mkdir -p $(BUILD)
 
-$(BUILD)/bdpt_kernels.o: $(CSRC)/bdpt_kernels.hip $(CSRC)/bdpt_device.h | $(BUILD)
+$(BUILD)/bdpt_kernels.o: $(CSRC)/bdpt_kernels.hip $(CSRC)/bdpt_device.h $(CSRC)/bdpt_math.h | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(BUILD)/bdpt_host.o: $(CSRC)/bdpt_host.cpp $(CSRC)/bdpt_device.h include/bdpt.h | $(BUILD)
@@ -32,6 +33,7 @@ $(BUILD)/bdpt_util.o: $(CSRC)/bdpt_util.c include/bdpt.h | $(BUILD)
 	$(CC) $(CFLAGS) -c $< -o $@
 
 $(LIB): $(BUILD)/bdpt_kernels.o $(BUILD)/bdpt_host.o $(BUILD)/bdpt_util.o
+	mkdir -p $(dir $(LIB))
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lm
 
 $(HOST): $(CSRC)/smallpt.c include/bdpt.h $(LIB)
@@ -43,4 +45,8 @@ $(ORACLE): oracle/bdpt_oracle.c include/bdpt.h
 clean:
 	rm -rf $(BUILD) $(LIB) $(HOST) $(ORACLE)
 
-.PHONY: all clean
+# A/B variants for the GPU bench harness: make variant NAME=x EXTRA_HIPFLAGS="..."
+variant:
+	$(MAKE) BUILD=variants/$(NAME)/_build LIB=variants/$(NAME)/libbdpt.so variants/$(NAME)/libbdpt.so
+
+.PHONY: all clean variant

@@ -8,7 +8,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libbdpt.so")
+LIB_PATH = os.environ.get("BDPT_LIB") or os.path.join(_HERE, "libbdpt.so")   # BDPT_LIB: A/B builds
 REPO_ROOT = os.path.dirname(_HERE)
 DEFAULT_DAT = os.path.join(REPO_ROOT, "assets", "data", "MersenneTwister.dat")
 SCENE_DIR = os.path.join(REPO_ROOT, "assets", "scenes")

@@ -354,14 +354,16 @@ int bdpt_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int npass
     const long per_pass = (long)c->W * c->H;
     int chunk = (int)((1L << 28) / (per_pass > 0 ? per_pass : 1));
     if (chunk < 1) chunk = 1;
-    if (chunk > 256) chunk = 256;
+    if (chunk > 128) chunk = 128;
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     int launches = 0;
     for (int p0 = 0; p0 < npass; p0 += chunk, launches++) {
         a.sid = c->d_sid + p0;
         a.vlp = c->d_vlp + p0;
         a.npass = npass - p0 < chunk ? npass - p0 : chunk;
-        const size_t smem = sizeof(float4) * (4 * (size_t)a.n + 3 * (size_t)a.npass) + sizeof(unsigned) * a.npass;
+        // spheres (4 tables) + per-pass VLPs + camera + 4 wave shadow queues + results + sids
+        const size_t smem = sizeof(float4) * (4 * (size_t)a.n + 3 * (size_t)a.npass + 5 + 4 * 128 * 2)
+                            + sizeof(unsigned) * (4 * 128 + (size_t)a.npass);
         if (smem > 160 * 1024)
             return fail(c, BDPT_EINVAL, "bdpt_path_passes: scene too large for LDS (%u spheres)", a.n);
         void* kargs[] = {&a};

@@ -42,17 +42,18 @@ __device__ __forceinline__ void sincos_cr(float x, float* s, float* c) {
     *c = (float)cd;
 }
 
-// SphereIntersectDevice device.cu:80-104 (g = {p.x, p.y, p.z, rad*rad}).
+// SphereIntersectDevice device.cu:80-104 (g = {p.x, p.y, p.z, rad*rad}), branch-free.
+// For 0 <= det < 2^-96 the root is not correctly rounded, but it is < 2^-47: then either
+// |b| >= 2^-23 and fl(b -+ root) == b == fl(b -+ sqrtf(det)), or both roots are < EPSILON and the
+// test returns 0 -- the result equals the reference's for every det.
 __device__ __forceinline__ float sphere_isect(float4 g, f3 o, f3 d) {
     f3 op = mk(g.x - o.x, g.y - o.y, g.z - o.z);
     float b = dot(op, d);
     float det = b * b - dot(op, op) + g.w;
-    if (det < 0.f) return 0.f;
-    det = bdpt_sqrt_rn(det);
-    float t = b - det;
-    if (t > kEps) return t;
-    t = b + det;
-    return t > kEps ? t : 0.f;
+    const float s = bdpt_sqrt_rn_core(det);
+    const float t1 = b - s, t2 = b + s;
+    const float r = t1 > kEps ? t1 : (t2 > kEps ? t2 : 0.f);
+    return det < 0.f ? 0.f : r;
 }
 
 // UniformSampleSphereDevice device.cu:157-165
@@ -194,18 +195,37 @@ extern "C" __global__ __launch_bounds__(64) void bdpt_light_kernel(const bdpt_de
 //  * Path regeneration: one loop iteration = one path segment for every live lane; a lane whose
 //    path ends accumulates and starts its next pass in the next iteration, so lanes never idle
 //    waiting for the longest path of the wave (the reference's 1-spp launch idles them).
-//  * Sphere geometry {p, rad^2}: for N = 1..16 spheres (template) it is loaded once into SGPRs and
-//    every traversal loop is fully unrolled; otherwise (N = 0) it is staged in LDS and read as a
-//    wave-uniform broadcast.  Emission / colour / material / centre for the per-lane hit id are
-//    LDS tables; the per-pass sid and VLP (the reference's dev_lp[vlp_index]) are LDS tables too.
+//  * Shadow-ray compaction: the NEE and VLP shadow rays of the wave's diffuse vertices
+//    (SampleLightsDevice :457-542) are pushed into a per-wave LDS queue at positions given by a
+//    ballot + mbcnt prefix count, then traced by all 64 lanes in a wave-uniform pass (1 pass for
+//    <= 64 rays, 2 for <= 128) instead of two half-empty divergent loops.  The main loop is
+//    wave-uniform (lanes with no work left still serve the queue).
+//  * Sphere geometry {p, rad^2}: for N = 1..16 spheres (template) it is read through wave-uniform
+//    scalar loads and every traversal loop is fully unrolled; otherwise (N = 0) it is staged in
+//    LDS.  Emission / colour / material / centre for the per-lane hit id, the per-pass sid and
+//    VLP (dev_lp[vlp_index]) and the camera constants are LDS tables.
 //  * The 5 random numbers a segment may consume (d_Rand[j..j+4], j = (26+25i+5*depth+sid) mod
-//    (RAND_N-5), device.cu:619) are prefetched one segment ahead, so the L2/MALL gather latency
-//    hides behind the traversal of the current segment.
-//  * 256-thread workgroup = 16x16 pixel tile as 2x2 waves of 8x8 pixels (2-D tiles keep the
-//    paths of a wave coherent).
+//    (RAND_N-5), device.cu:619) are prefetched one segment ahead.
+//  * 256-thread workgroup = 16x16 pixel tile as 2x2 waves of 8x8 pixels.
 // =============================================================================================
+namespace {
+constexpr int kQueue = 128;                       // shadow rays per wave and step (<= 2 per lane)
+
+__device__ __forceinline__ int lane_prefix(unsigned long long mask) {
+    return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32),
+                                          __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
+}
+__device__ __forceinline__ void wave_lds_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+}  // namespace
+
+#ifndef BDPT_WAVES_PER_SIMD
+#define BDPT_WAVES_PER_SIMD 5
+#endif
 template <int N>
-__global__ __launch_bounds__(256) void bdpt_path_kernel_t(bdpt_path_args a) {
+__global__ __launch_bounds__(256, BDPT_WAVES_PER_SIMD) void bdpt_path_kernel_t(bdpt_path_args a) {
     extern __shared__ float4 smem[];
     const int n = N > 0 ? N : (int)a.n;
     constexpr int kUnroll = N > 0 ? N : 1;
@@ -214,7 +234,10 @@ __global__ __launch_bounds__(256) void bdpt_path_kernel_t(bdpt_path_args a) {
     float4* P = smem + 2 * n;         // {px, py, pz, 0}  (hit normal)
     float4* G = smem + 3 * n;         // {px, py, pz, rad^2}  (N == 0 traversal)
     float4* V = smem + 4 * n;         // per pass: VLP {hx,hy,hz,rx}{ry,rz,nx,ny}{nz,-,-,-}
-    unsigned* SID = (unsigned*)(V + 3 * a.npass);
+    float4* K = V + 3 * a.npass;      // camera constants (5 float4)
+    float4* Q = K + 5;                // shadow queues: 4 waves x kQueue x 2 float4
+    unsigned* R = (unsigned*)(Q + 4 * kQueue * 2);    // shadow results: 4 x kQueue
+    unsigned* SID = R + 4 * kQueue;   // per pass sid
     for (int s = threadIdx.x; s < n; s += 256) {
         const bdpt_dev_sphere S = a.sph[s];
         const bool emis = !(S.ex == 0.f && S.ey == 0.f && S.ez == 0.f);
@@ -230,28 +253,21 @@ __global__ __launch_bounds__(256) void bdpt_path_kernel_t(bdpt_path_args a) {
         V[3 * q + 2] = make_float4(L.nz, 0.f, 0.f, 0.f);
         SID[q] = a.sid[q];
     }
+    if (threadIdx.x == 0) {
+        K[0] = make_float4(a.ux[0], a.ux[1], a.ux[2], a.tx);
+        K[1] = make_float4(a.uy[0], a.uy[1], a.uy[2], a.ty);
+        K[2] = make_float4(a.ud[0], a.ud[1], a.ud[2], a.tz);
+        K[3] = make_float4(a.orig[0], a.orig[1], a.orig[2], 0.f);
+        K[4] = make_float4(a.inv_w, a.inv_h, 0.f, 0.f);
+    }
     __syncthreads();
 
-    float4 g[N > 0 ? N : 1];
-    if constexpr (N > 0) {
-#pragma unroll
-        for (int s = 0; s < N; s++) g[s] = a.geom[s];           // wave-uniform: SGPRs
-    }
     auto geom = [&](int s) -> float4 {
-        if constexpr (N > 0) return g[s]; else return G[s];
+        if constexpr (N > 0) return a.geom[s]; else return G[s];
     };
     auto emissive = [&](int s) -> bool {
         if constexpr (N > 0) return (a.emis_mask >> s) & 1u;
         else return (__float_as_int(C[s].w) & 256) != 0;
-    };
-    // IntersectPDevice / IntersectPVacuumDevice (device.cu:126-154): any hit in (0, maxt)
-    auto occluded = [&](f3 o, f3 d, float maxt, bool vacuum) -> bool {
-#pragma unroll kUnroll
-        for (int s = n - 1; s >= 0; --s) {
-            const float dd = sphere_isect(geom(s), o, d);
-            if (dd != 0.f && dd < maxt && !(vacuum && emissive(s))) return true;
-        }
-        return false;
     };
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -259,180 +275,241 @@ __global__ __launch_bounds__(256) void bdpt_path_kernel_t(bdpt_path_args a) {
     const int y = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
     bool active = x < a.W && y < a.H;
     if (active && a.nshards > 1) active = ((y / a.band_rows) % a.nshards) == a.shard;
-    if (!active) return;
+    float4* SQ = Q + wave * kQueue * 2;
+    unsigned* SR = R + wave * kQueue;
 
-    const int i = y * a.W + x;
+    const int i = active ? y * a.W + x : 0;
     const unsigned ibase = 26u + (unsigned)(i * 25);
     const float* __restrict__ rnd = a.rnd;
     constexpr unsigned M5 = kRandN - 5u;
 
-    bdpt_dev_vec cv = a.colors[i];
-    f3 col = mk(cv.x, cv.y, cv.z);
-    unsigned cnt = a.counter[i];
+    f3 col = mk(0.f, 0.f, 0.f);
+    unsigned cnt = 0;
+    if (active) {
+        const bdpt_dev_vec cv = a.colors[i];
+        col = mk(cv.x, cv.y, cv.z);
+        cnt = a.counter[i];
+    }
     const unsigned cnt0 = cnt;
-
-    const f3 ux = mk(a.ux[0], a.ux[1], a.ux[2]);
-    const f3 uy = mk(a.uy[0], a.uy[1], a.uy[2]);
-    const f3 ud = mk(a.ud[0], a.ud[1], a.ud[2]);
-    const f3 org = mk(a.orig[0], a.orig[1], a.orig[2]);
-    const double kx0 = (double)((float)x * a.inv_w) - a.half_w;   // device.cu:565-566
-    const double ky0 = (double)((float)y * a.inv_h) - a.half_h;
+    const float4 k4 = K[4];
+    const double kx0 = (double)((float)x * k4.x) - a.half_w;   // device.cu:565-566
+    const double ky0 = (double)((float)y * k4.y) - a.half_h;
 
     int p = 0;
     unsigned depth = 0, sid = SID[0];
     unsigned j = (ibase + sid) % M5;
     float q0 = rnd[j], q1 = rnd[j + 1], q2 = rnd[j + 2], q3 = rnd[j + 3], q4 = rnd[j + 4];
-    f3 ro = mk(0.f, 0.f, 0.f), rd = ro, thr = ro, rad = ro;
+    f3 ro = mk(0.f, 0.f, 0.f), rd = ro, thr = ro, rad = ro, nl = ro;
     bool specular = true, fresh = true;
+    bool alive = active && p < a.npass && cnt < BDPT_DEV_COUNTER_CAP;
 
-    while (p < a.npass && cnt < BDPT_DEV_COUNTER_CAP) {
-        if (fresh) {                          // camera ray (:562-600); d_Rand[kk] == q0 (kk == j)
-            const float kx = (float)(kx0 + (double)(q0 * a.inv_w));
-            const float ky = (float)(ky0 + (double)(q1 * a.inv_h));
-            const float kz = 10.0f;
-            f3 rdir = mk(0.f, 0.f, 0.f);
-            rdir = add(rdir, smul(kx, ux));
-            rdir = add(rdir, smul(ky, uy));
-            rdir = add(rdir, smul(kz, ud));
-            const float w = (a.tx * kx + a.ty * ky + a.tz * kz) + 1;
-            rdir = smul((float)(1. / (double)w), rdir);
-            ro = add(rdir, org);
-            rd = norm(rdir);
-            rad = mk(0.f, 0.f, 0.f);
-            thr = mk(1.f, 1.f, 1.f);
-            specular = true;
-            fresh = false;
-        }
-
-        // closest hit, scanning from the last sphere down (device.cu:106-124)
-        float t = 1e20f;
-        int id = -1;
+    while (__builtin_amdgcn_ballot_w64(alive) != 0) {                   // wave-uniform loop
+        bool done = false, diff = false;
+        if (alive) {
+            if (fresh) {                  // camera ray (:562-600); d_Rand[kk] == q0 (kk == j)
+                const float4 c0 = K[0], c1 = K[1], c2 = K[2], c3 = K[3];
+                const float kx = (float)(kx0 + (double)(q0 * k4.x));
+                const float ky = (float)(ky0 + (double)(q1 * k4.y));
+                const float kz = 10.0f;
+                f3 rdir = mk(0.f, 0.f, 0.f);
+                rdir = add(rdir, smul(kx, mk(c0.x, c0.y, c0.z)));
+                rdir = add(rdir, smul(ky, mk(c1.x, c1.y, c1.z)));
+                rdir = add(rdir, smul(kz, mk(c2.x, c2.y, c2.z)));
+                const float w = (c0.w * kx + c1.w * ky + c2.w * kz) + 1;
+                rdir = smul((float)(1. / (double)w), rdir);
+                ro = add(rdir, mk(c3.x, c3.y, c3.z));
+                rd = norm(rdir);
+                rad = mk(0.f, 0.f, 0.f);
+                thr = mk(1.f, 1.f, 1.f);
+                specular = true;
+                fresh = false;
+            }
+            // closest hit, scanning from the last sphere down (device.cu:106-124)
+            float t = 1e20f;
+            int id = -1;
 #pragma unroll kUnroll
-        for (int s = n - 1; s >= 0; --s) {
-            const float d = sphere_isect(geom(s), ro, rd);
-            if (d != 0.f && d < t) { t = d; id = s; }
-        }
-        bool done = id < 0;
-        if (!done) {
-            const float4 cm = C[id];
-            const int mat = __float_as_int(cm.w);
-            const float4 pc = P[id];
-            const f3 hit = add(ro, smul(t, rd));
-            const f3 normal = norm(sub(hit, mk(pc.x, pc.y, pc.z)));
-            const float dp = dot(normal, rd);
-            const f3 nl = smul(-1.f * (float)(dp > 0 ? 1 : -1), normal);
-            if (mat & 256) {                                             // emitter (:651-661)
-                if (specular) {
-                    const float4 em = E[id];
-                    rad = add(rad, mul(thr, smul(fabsf(dp), mk(em.x, em.y, em.z))));
-                }
-                done = true;
-            } else if ((mat & 255) == BDPT_DEV_DIFF) {                   // :663-703
-                specular = false;
-                thr = mul(thr, mk(cm.x, cm.y, cm.z));
-                // SampleLightsDevice(.., nn = j+2) device.cu:457-542: d_Rand[j+3], d_Rand[j+4]
-                f3 res = mk(0.f, 0.f, 0.f);
-                if (a.n_lights) {
-                    const f3 usp = uniform_sphere(q3, q4);               // same for every light
-                    for (unsigned li = 0; li < a.n_lights; li++) {
-                        const float4 lg = a.lightrec[2 * li];             // {p, rad}
-                        const float4 le = a.lightrec[2 * li + 1];         // {e, 4*pi*rad*rad}
-                        const f3 spt = add(smul(lg.w, usp), mk(lg.x, lg.y, lg.z));
-                        f3 sd = sub(spt, hit);
-                        const float len = bdpt_sqrt_rn(dot(sd, sd));
-                        sd = smul(1.f / len, sd);
-                        float wo = dot(sd, usp);
-                        if (wo > 0.f) continue;
-                        wo = -wo;
-                        const float wi = dot(sd, nl);
-                        if (wi > 0.f && !occluded(hit, sd, len - kEps, false)) {
-                            const float sc = le.w * wi * wo / (len * len);
-                            res = add(res, smul(sc, mk(le.x, le.y, le.z)));
+            for (int s = n - 1; s >= 0; --s) {
+                const float d = sphere_isect(geom(s), ro, rd);
+                if (d != 0.f && d < t) { t = d; id = s; }
+            }
+            done = id < 0;
+            if (!done) {
+                const float4 cm = C[id];
+                const int mat = __float_as_int(cm.w);
+                const float4 pc = P[id];
+                const f3 hit = add(ro, smul(t, rd));
+                const f3 normal = norm(sub(hit, mk(pc.x, pc.y, pc.z)));
+                const float dp = dot(normal, rd);
+                nl = smul(-1.f * (float)(dp > 0 ? 1 : -1), normal);
+                if (mat & 256) {                                         // emitter (:651-661)
+                    if (specular) {
+                        const float4 em = E[id];
+                        rad = add(rad, mul(thr, smul(fabsf(dp), mk(em.x, em.y, em.z))));
+                    }
+                    done = true;
+                } else if ((mat & 255) == BDPT_DEV_DIFF) {               // :663-703
+                    specular = false;
+                    thr = mul(thr, mk(cm.x, cm.y, cm.z));
+                    diff = true;                  // shadow rays: below, compacted over the wave
+                    ro = hit;
+                    rd = cosine_dir(nl, q0, q1);
+                } else if ((mat & 255) == BDPT_DEV_SPEC) {               // :704-714
+                    specular = true;
+                    const f3 nd = sub(rd, smul(2.f * dot(normal, rd), normal));
+                    thr = mul(thr, mk(cm.x, cm.y, cm.z));
+                    ro = hit;
+                    rd = nd;
+                } else {                                                 // REFR / LITE :715-770
+                    specular = true;
+                    const f3 refl = sub(rd, smul(2.f * dot(normal, rd), normal));
+                    const bool into = dot(normal, nl) > 0;
+                    const float nc = 1.f, nt = 1.5f;
+                    const float nnt = into ? nc / nt : nt / nc;
+                    const float ddn = dot(rd, nl);
+                    const float cos2t = 1.f - nnt * nnt * (1.f - ddn * ddn);
+                    if (cos2t < 0.f) {
+                        thr = mul(thr, mk(cm.x, cm.y, cm.z));
+                        rd = refl;
+                    } else {
+                        const float kq = (float)(into ? 1 : -1) * (ddn * nnt + bdpt_sqrt_rn(cos2t));
+                        const f3 td = norm(sub(smul(nnt, rd), smul(kq, normal)));
+                        const float aa = nt - nc, bb = nt + nc;
+                        const float R0 = aa * aa / (bb * bb);
+                        const float c = 1 - (into ? -ddn : dot(td, normal));
+                        const float Re = R0 + (1 - R0) * c * c * c * c * c;
+                        const float Tr = 1.f - Re;
+                        const float Pp = .25f + .5f * Re;
+                        const float RP = Re / Pp;
+                        const float TP = Tr / (1.f - Pp);
+                        if (q2 < Pp) {
+                            thr = mul(smul(RP, thr), mk(cm.x, cm.y, cm.z));
+                            rd = refl;
+                        } else {
+                            thr = mul(smul(TP, thr), mk(cm.x, cm.y, cm.z));
+                            rd = td;
                         }
                     }
+                    ro = hit;
                 }
-                f3 vres = mk(0.f, 0.f, 0.f);
-                {
-                    const float4 v0 = V[3 * p], v1 = V[3 * p + 1], v2 = V[3 * p + 2];
-                    f3 sd = sub(mk(v0.x, v0.y, v0.z), hit);
+            }
+        }
+
+        // ---- SampleLightsDevice (device.cu:457-542) for the diffuse vertices of this segment:
+        // NEE towards every emitter (same d_Rand[j+3], d_Rand[j+4] for all) + 1 VLP, blended 1/2.
+        if (__builtin_amdgcn_ballot_w64(diff) != 0) {
+            f3 res = mk(0.f, 0.f, 0.f), usp = res, vsd = res, vcon = res;
+            if (diff) usp = uniform_sphere(q3, q4);
+            const int nsteps = a.n_lights > 0 ? (int)a.n_lights : 1;
+            for (int li = 0; li < nsteps; li++) {                         // uniform
+                bool has_nee = false, has_vlp = false;
+                f3 sd = res, con = res;
+                float maxt = 0.f, vmaxt = 0.f;
+                if (diff && a.n_lights > 0) {
+                    const float4 lg = a.lightrec[2 * li];                 // {p, rad}
+                    const float4 le = a.lightrec[2 * li + 1];             // {e, 4*pi*rad*rad}
+                    const f3 spt = add(smul(lg.w, usp), mk(lg.x, lg.y, lg.z));
+                    sd = sub(spt, ro);
                     const float len = bdpt_sqrt_rn(dot(sd, sd));
                     sd = smul(1.f / len, sd);
-                    float wo = dot(sd, mk(v1.z, v1.w, v2.x));
+                    float wo = dot(sd, usp);
                     if (!(wo > 0.f)) {
                         wo = -wo;
                         const float wi = dot(sd, nl);
-                        if (wi > 0.f && !occluded(hit, sd, len - kEps, true))
-                            vres = add(vres, smul(wi * wo, mk(v0.w, v1.x, v1.y)));
+                        if (wi > 0.f) {
+                            has_nee = true;
+                            maxt = len - kEps;
+                            con = smul(le.w * wi * wo / (len * len), mk(le.x, le.y, le.z));
+                        }
                     }
                 }
+                if (diff && li == 0) {                                    // the VLP (:507-537)
+                    const float4 v0 = V[3 * p], v1 = V[3 * p + 1], v2 = V[3 * p + 2];
+                    vsd = sub(mk(v0.x, v0.y, v0.z), ro);
+                    const float len = bdpt_sqrt_rn(dot(vsd, vsd));
+                    vsd = smul(1.f / len, vsd);
+                    float wo = dot(vsd, mk(v1.z, v1.w, v2.x));
+                    if (!(wo > 0.f)) {
+                        wo = -wo;
+                        const float wi = dot(vsd, nl);
+                        if (wi > 0.f) {
+                            has_vlp = true;
+                            vmaxt = len - kEps;
+                            vcon = smul(wi * wo, mk(v0.w, v1.x, v1.y));
+                        }
+                    }
+                }
+                // compact this step's shadow rays into the wave's queue
+                const unsigned long long mn = __builtin_amdgcn_ballot_w64(has_nee);
+                const unsigned long long mv = __builtin_amdgcn_ballot_w64(has_vlp);
+                const int cn = __popcll(mn);
+                const int total = cn + __popcll(mv);
+                const int pn = lane_prefix(mn), pv = cn + lane_prefix(mv);
+                if (has_nee) {                    // SoA: {o, maxt}[kQueue], {d, vacuum}[kQueue]
+                    SQ[pn] = make_float4(ro.x, ro.y, ro.z, maxt);
+                    SQ[kQueue + pn] = make_float4(sd.x, sd.y, sd.z, 0.f);
+                }
+                if (has_vlp) {
+                    SQ[pv] = make_float4(ro.x, ro.y, ro.z, vmaxt);
+                    SQ[kQueue + pv] = make_float4(vsd.x, vsd.y, vsd.z, 1.f);
+                }
+                wave_lds_fence();
+                for (int base = 0; base < total; base += 64) {            // uniform
+                    const int idx = base + lane;
+                    if (idx < total) {
+                        const float4 r0 = SQ[idx], r1 = SQ[kQueue + idx];
+                        const f3 o = mk(r0.x, r0.y, r0.z), d = mk(r1.x, r1.y, r1.z);
+                        const bool vac = r1.w != 0.f;
+                        unsigned occ = 0;
+#pragma unroll kUnroll
+                        for (int s = n - 1; s >= 0; --s) {                // IntersectP(Vacuum)Device
+                            const float dd = sphere_isect(geom(s), o, d);
+                            if (dd != 0.f && dd < r0.w && !(vac && emissive(s))) { occ = 1; break; }
+                        }
+                        SR[idx] = occ;
+                    }
+                }
+                wave_lds_fence();
+                if (has_nee && SR[pn] == 0) res = add(res, con);
+                if (has_vlp && SR[pv] != 0) vcon = mk(0.f, 0.f, 0.f);
+                if (li == 0 && !has_vlp) vcon = mk(0.f, 0.f, 0.f);
+                wave_lds_fence();
+            }
+            if (diff) {
+                f3 vres = mk(0.f, 0.f, 0.f);
+                vres = add(vres, vcon);
                 vres = smul(1.f, vres);
                 res = add(res, vres);
                 res = smul(0.5f, res);
                 rad = add(rad, mul(res, thr));
-                ro = hit;
-                rd = cosine_dir(nl, q0, q1);
-            } else if ((mat & 255) == BDPT_DEV_SPEC) {                   // :704-714
-                specular = true;
-                const f3 nd = sub(rd, smul(2.f * dot(normal, rd), normal));
-                thr = mul(thr, mk(cm.x, cm.y, cm.z));
-                ro = hit;
-                rd = nd;
-            } else {                                                     // REFR / LITE :715-770
-                specular = true;
-                const f3 refl = sub(rd, smul(2.f * dot(normal, rd), normal));
-                const bool into = dot(normal, nl) > 0;
-                const float nc = 1.f, nt = 1.5f;
-                const float nnt = into ? nc / nt : nt / nc;
-                const float ddn = dot(rd, nl);
-                const float cos2t = 1.f - nnt * nnt * (1.f - ddn * ddn);
-                if (cos2t < 0.f) {
-                    thr = mul(thr, mk(cm.x, cm.y, cm.z));
-                    ro = hit;
-                    rd = refl;
-                } else {
-                    const float kq = (float)(into ? 1 : -1) * (ddn * nnt + bdpt_sqrt_rn(cos2t));
-                    const f3 td = norm(sub(smul(nnt, rd), smul(kq, normal)));
-                    const float aa = nt - nc, bb = nt + nc;
-                    const float R0 = aa * aa / (bb * bb);
-                    const float c = 1 - (into ? -ddn : dot(td, normal));
-                    const float Re = R0 + (1 - R0) * c * c * c * c * c;
-                    const float Tr = 1.f - Re;
-                    const float Pp = .25f + .5f * Re;
-                    const float RP = Re / Pp;
-                    const float TP = Tr / (1.f - Pp);
-                    if (q2 < Pp) {
-                        thr = mul(smul(RP, thr), mk(cm.x, cm.y, cm.z));
-                        rd = refl;
-                    } else {
-                        thr = mul(smul(TP, thr), mk(cm.x, cm.y, cm.z));
-                        rd = td;
-                    }
-                    ro = hit;
-                }
             }
+        }
+
+        if (alive) {
             if (!done && ++depth > 6) done = true;                       // :621 7-segment cap
-        }
-        if (done) {                                                      // :774-787
-            if (cnt == 0) {
-                col = rad;
-            } else {
-                const float k1 = (float)cnt;
-                const float k2 = 1.f / (k1 + 1.f);
-                col.x = (col.x * k1 + rad.x) * k2;
-                col.y = (col.y * k1 + rad.y) * k2;
-                col.z = (col.z * k1 + rad.z) * k2;
+            if (done) {                                                  // :774-787
+                if (cnt == 0) {
+                    col = rad;
+                } else {
+                    const float k1 = (float)cnt;
+                    const float k2 = 1.f / (k1 + 1.f);
+                    col.x = (col.x * k1 + rad.x) * k2;
+                    col.y = (col.y * k1 + rad.y) * k2;
+                    col.z = (col.z * k1 + rad.z) * k2;
+                }
+                cnt++;
+                p++;
+                fresh = true;
+                depth = 0;
+                alive = p < a.npass && cnt < BDPT_DEV_COUNTER_CAP;
+                if (alive) sid = SID[p];
             }
-            cnt++;
-            p++;
-            fresh = true;
-            depth = 0;
-            if (p < a.npass) sid = SID[p];
+            if (alive) {                  // prefetch the next segment's random numbers (:619)
+                j = (ibase + depth * 5u + sid) % M5;
+                q0 = rnd[j]; q1 = rnd[j + 1]; q2 = rnd[j + 2]; q3 = rnd[j + 3]; q4 = rnd[j + 4];
+            }
         }
-        // prefetch the random numbers of the next segment (device.cu:619)
-        j = (ibase + depth * 5u + sid) % M5;
-        q0 = rnd[j]; q1 = rnd[j + 1]; q2 = rnd[j + 2]; q3 = rnd[j + 3]; q4 = rnd[j + 4];
     }
-    if (cnt == cnt0) return;                                             // nothing rendered
+    if (!active || cnt == cnt0) return;                                  // nothing rendered
     bdpt_dev_vec out;
     out.x = col.x; out.y = col.y; out.z = col.z;
     a.colors[i] = out;

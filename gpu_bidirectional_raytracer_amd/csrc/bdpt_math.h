@@ -44,8 +44,8 @@ BDPT_HD void bdpt_sincos_dp(double x, double* so, double* co) {
 }
 
 #if defined(__HIPCC__)
-__device__ __forceinline__ float bdpt_sqrt_rn(float x) {
-    if (__builtin_expect(!(x >= 0x1p-96f), 0)) return sqrtf(x);
+// v_sqrt_f32 + the +-1 ulp residual correction: correctly rounded for x >= 2^-96 and x == 0.
+__device__ __forceinline__ float bdpt_sqrt_rn_core(float x) {
     float s = __builtin_amdgcn_sqrtf(x);
     const float sdn = __int_as_float(__float_as_int(s) - 1);
     const float sup = __int_as_float(__float_as_int(s) + 1);
@@ -54,6 +54,11 @@ __device__ __forceinline__ float bdpt_sqrt_rn(float x) {
     s = rdn <= 0.f ? sdn : s;
     s = rup > 0.f ? sup : s;
     return s;
+}
+
+__device__ __forceinline__ float bdpt_sqrt_rn(float x) {
+    if (__builtin_expect(!(x >= 0x1p-96f), 0)) return sqrtf(x);
+    return bdpt_sqrt_rn_core(x);
 }
 #endif
 

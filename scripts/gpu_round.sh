@@ -9,13 +9,18 @@ ok_or_stop() {  # $1 = exit code, $2 = step name; test failures (1) continue, fa
   if [ "$1" -ne 0 ] && [ "$1" -ne 1 ]; then echo "STOP after $2 (exit $1)"; exit "$1"; fi
 }
 STEPS="${STEPS:-tests bench prof}"
-PMC_SETS=(
+if [ -n "${PMC_MIX:-}" ]; then PMC_SETS=(
+  "SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64"
+  "SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT SQ_INSTS_VALU_FLOPS_FP32 SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_FLOPS_FP32_TRANS SQ_INSTS_VALU_IOPS SQ_INSTS_VALU"
+  "SQ_INSTS_LDS_LOAD SQ_INSTS_LDS_STORE SQ_INSTS_BRANCH SQ_INST_CYCLES_SALU SQ_INST_CYCLES_SMEM SQ_INSTS_VSKIPPED SQ_INSTS_SMEM SQ_INSTS_SALU"
+  "SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE"
+); else PMC_SETS=(
   "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM GRBM_GUI_ACTIVE"
   "SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT"
   "FETCH_SIZE"
   "WRITE_SIZE"
   "TCC_HIT_sum TCC_MISS_sum"
-)
+); fi
 for s in $STEPS; do
   case "$s" in
   tests)

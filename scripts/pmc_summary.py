@@ -1,0 +1,24 @@
+"""Summarise rocprofv3 --pmc CSVs for one kernel: python scripts/pmc_summary.py gpurun_out [kernel]."""
+import collections, csv, glob, os, sys
+
+root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
+kern = sys.argv[2] if len(sys.argv) > 2 else "path_kernel"
+vals = collections.defaultdict(list)
+for f in sorted(glob.glob(os.path.join(root, "pmc*", "run_counter_collection.csv"))):
+    for r in csv.DictReader(open(f)):
+        if kern in r["Kernel_Name"]:
+            vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
+m = {k: sum(v) / len(v) for k, v in vals.items()}
+for k in sorted(m):
+    print(f"{k:28s} {m[k]:.4g}")
+def g(k): return m.get(k, float("nan"))
+print("--- derived (per dispatch)")
+print(f"VALU lane utilisation      {g('SQ_THREAD_CYCLES_VALU') / (64 * g('SQ_ACTIVE_INST_VALU')):.3f}")
+print(f"wait / issue-stall / active {g('SQ_WAIT_ANY') / g('SQ_WAVE_CYCLES'):.3f} / "
+      f"{g('SQ_WAIT_INST_ANY') / g('SQ_WAVE_CYCLES'):.3f} / {g('SQ_ACTIVE_INST_ANY') / g('SQ_WAVE_CYCLES'):.3f}")
+cyc = g('GRBM_GUI_ACTIVE') / 8
+print(f"kernel cycles (per XCD)     {cyc:.4g}")
+print(f"VALU busy (instr*2/(4*256*cyc)) {g('SQ_INSTS_VALU') * 2 / (4 * 256 * cyc):.3f}")
+print(f"SALU / VALU instr           {g('SQ_INSTS_SALU') / g('SQ_INSTS_VALU'):.3f}")
+print(f"L2 hit rate                 {g('TCC_HIT_sum') / (g('TCC_HIT_sum') + g('TCC_MISS_sum')):.3f}")
+print(f"FETCH (MB) / WRITE (MB)     {g('FETCH_SIZE') / 1024:.1f} / {g('WRITE_SIZE') / 1024:.1f}")
