@@ -24,7 +24,12 @@ __device__ __forceinline__ f3 sub(f3 a, f3 b) { return mk(a.x - b.x, a.y - b.y, 
 __device__ __forceinline__ f3 mul(f3 a, f3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
 __device__ __forceinline__ f3 smul(float k, f3 b) { return mk(k * b.x, k * b.y, k * b.z); }
 __device__ __forceinline__ float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
-__device__ __forceinline__ f3 norm(f3 v) { float l = 1.f / bdpt_sqrt_rn(dot(v, v)); return smul(l, v); }
+__device__ __forceinline__ f3 norm(f3 v) {
+#ifdef BDPT_ABL_DIV
+    return smul(__builtin_amdgcn_rsqf(dot(v, v)), v);
+#endif
+    float l = 1.f / bdpt_sqrt_rn(dot(v, v)); return smul(l, v);
+}
 __device__ __forceinline__ f3 cross(f3 a, f3 b) {
     return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }
@@ -36,6 +41,9 @@ constexpr unsigned kRandN = BDPT_DEV_RAND_N;
 
 // sinf/cosf with correctly-rounded semantics: fp64 sincos rounded once to fp32 (bdpt_math.h).
 __device__ __forceinline__ void sincos_cr(float x, float* s, float* c) {
+#ifdef BDPT_ABL_SINCOS
+    *s = __sinf(x); *c = __cosf(x); return;
+#endif
     double sd, cd;
     bdpt_sincos_dp((double)x, &sd, &cd);
     *s = (float)sd;
@@ -54,6 +62,19 @@ __device__ __forceinline__ float sphere_isect(float4 g, f3 o, f3 d) {
     const float t1 = b - s, t2 = b + s;
     const float r = t1 > kEps ? t1 : (t2 > kEps ? t2 : 0.f);
     return det < 0.f ? 0.f : r;
+}
+
+// The same test with "no hit" encoded as +inf instead of 0, so the closest-hit update is one
+// compare (d < t) and the any-hit test is d < maxt.  t1 > EPS ? t1 : (t2 > EPS ? t2 : miss) ==
+// (r = t1 > EPS ? t1 : t2) > EPS ? r : miss; det < 0 (or NaN) -> miss, as in the reference.
+__device__ __forceinline__ float sphere_isect_inf(float4 g, f3 o, f3 d) {
+    f3 op = mk(g.x - o.x, g.y - o.y, g.z - o.z);
+    float b = dot(op, d);
+    float det = b * b - dot(op, op) + g.w;
+    const float s = bdpt_sqrt_rn_core(det);
+    const float t1 = b - s, t2 = b + s;
+    const float r = t1 > kEps ? t1 : t2;
+    return (r > kEps && det >= 0.f) ? r : __builtin_inff();
 }
 
 // UniformSampleSphereDevice device.cu:157-165
@@ -316,7 +337,9 @@ __global__ __launch_bounds__(256, BDPT_WAVES_PER_SIMD) void bdpt_path_kernel_t(b
                 rdir = add(rdir, smul(ky, mk(c1.x, c1.y, c1.z)));
                 rdir = add(rdir, smul(kz, mk(c2.x, c2.y, c2.z)));
                 const float w = (c0.w * kx + c1.w * ky + c2.w * kz) + 1;
-                rdir = smul((float)(1. / (double)w), rdir);
+                // (float)(1./(double)w) == 1.f/w: double rounding of a quotient is innocuous
+                // when 53 >= 2*24 + 2 (device.cu:594)
+                rdir = smul(1.f / w, rdir);
                 ro = add(rdir, mk(c3.x, c3.y, c3.z));
                 rd = norm(rdir);
                 rad = mk(0.f, 0.f, 0.f);
@@ -329,8 +352,8 @@ __global__ __launch_bounds__(256, BDPT_WAVES_PER_SIMD) void bdpt_path_kernel_t(b
             int id = -1;
 #pragma unroll kUnroll
             for (int s = n - 1; s >= 0; --s) {
-                const float d = sphere_isect(geom(s), ro, rd);
-                if (d != 0.f && d < t) { t = d; id = s; }
+                const float d = sphere_isect_inf(geom(s), ro, rd);
+                if (d < t) { t = d; id = s; }
             }
             done = id < 0;
             if (!done) {
@@ -340,7 +363,7 @@ __global__ __launch_bounds__(256, BDPT_WAVES_PER_SIMD) void bdpt_path_kernel_t(b
                 const f3 hit = add(ro, smul(t, rd));
                 const f3 normal = norm(sub(hit, mk(pc.x, pc.y, pc.z)));
                 const float dp = dot(normal, rd);
-                nl = smul(-1.f * (float)(dp > 0 ? 1 : -1), normal);
+                nl = dp > 0 ? mk(-normal.x, -normal.y, -normal.z) : normal;   // (-1*sign(dp))*n, exact
                 if (mat & 256) {                                         // emitter (:651-661)
                     if (specular) {
                         const float4 em = E[id];
@@ -460,10 +483,14 @@ __global__ __launch_bounds__(256, BDPT_WAVES_PER_SIMD) void bdpt_path_kernel_t(b
                         const f3 o = mk(r0.x, r0.y, r0.z), d = mk(r1.x, r1.y, r1.z);
                         const bool vac = r1.w != 0.f;
                         unsigned occ = 0;
+#ifdef BDPT_ABL_SHADOW
+                        occ = r0.w < -1e30f || vac;
+                        if (0)
+#endif
 #pragma unroll kUnroll
                         for (int s = n - 1; s >= 0; --s) {                // IntersectP(Vacuum)Device
-                            const float dd = sphere_isect(geom(s), o, d);
-                            if (dd != 0.f && dd < r0.w && !(vac && emissive(s))) { occ = 1; break; }
+                            const float dd = sphere_isect_inf(geom(s), o, d);
+                            if (dd < r0.w && !(vac && emissive(s))) { occ = 1; break; }
                         }
                         SR[idx] = occ;
                     }

@@ -46,6 +46,9 @@ BDPT_HD void bdpt_sincos_dp(double x, double* so, double* co) {
 #if defined(__HIPCC__)
 // v_sqrt_f32 + the +-1 ulp residual correction: correctly rounded for x >= 2^-96 and x == 0.
 __device__ __forceinline__ float bdpt_sqrt_rn_core(float x) {
+#ifdef BDPT_ABL_SQRT
+    return __builtin_amdgcn_sqrtf(x);
+#endif
     float s = __builtin_amdgcn_sqrtf(x);
     const float sdn = __int_as_float(__float_as_int(s) - 1);
     const float sup = __int_as_float(__float_as_int(s) + 1);
