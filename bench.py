@@ -93,6 +93,7 @@ def main():
     import torch
 
     import gpu_bidirectional_raytracer_amd as g
+    from gpu_bidirectional_raytracer_amd import sharding as shd
 
     torch.cuda.set_device(local)
     dist = None
@@ -125,17 +126,9 @@ def main():
     r.path_timing(reset=True)
 
     # RCCL reduce target: torch tensors over the library's own device buffers (no copy)
-    col_ptr, cnt_ptr, _ = r.device_buffers()
-
-    class _Dev:
-        def __init__(self, ptr, n, typestr):
-            self.__cuda_array_interface__ = {"shape": (n,), "typestr": typestr,
-                                             "data": (ptr, False), "version": 3}
-
     t_col = t_cnt = None
     if dist is not None:
-        t_col = torch.as_tensor(_Dev(col_ptr, W * H * 3, "<f4"), device=f"cuda:{local}")
-        t_cnt = torch.as_tensor(_Dev(cnt_ptr, W * H, "<i4"), device=f"cuda:{local}")
+        t_col, t_cnt = shd.device_tensors(r, f"cuda:{local}")
 
     barrier()
     torch.cuda.synchronize()
@@ -144,8 +137,7 @@ def main():
         step(k)
     r.synchronize()
     if dist is not None:                                      # assemble the frame on rank 0
-        dist.reduce(t_col, dst=0, op=dist.ReduceOp.SUM)
-        dist.reduce(t_cnt, dst=0, op=dist.ReduceOp.SUM)
+        shd.reduce_frame(t_col, t_cnt, dst=0)
     torch.cuda.synchronize()
     barrier()
     dt = time.perf_counter() - t0
@@ -163,9 +155,7 @@ def main():
             r.update_pixels()
             cnt = t_cnt.cpu().numpy()
             assert (cnt == per_step * (args.warmup + args.steps)).all(), "reduced counters wrong"
-        own_pixels = W * H // world if world == 1 else int(
-            sum(W * (min(H, y0 + args.band_rows) - y0) for y0 in range(0, H, args.band_rows)
-                if (y0 // args.band_rows) % world == rank))
+        own_pixels = shd.owned_pixels(W, H, rank, world, args.band_rows)
         w = WORK.get(args.scene)
         avg_launch_s = dev_ms / 1e3 / max(launches, 1)
         passes_per_launch = per_step * args.steps / max(launches, 1)

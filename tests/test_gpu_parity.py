@@ -239,3 +239,38 @@ def test_smallpt_mirror_and_host_program(gpu, tmp_path):
                            os.path.join(REPO, "assets", "data", "MersenneTwister.dat")], cwd=tmp_path)
     assert open(ppm_py).read() == out.read_text()
     spt.FreeBuffers()
+
+
+def test_rccl_frame_assembly_world1(gpu):
+    """bench.py's N>1 assembly path on one GPU: torch tensors aliasing libbdpt's device buffers
+    (__cuda_array_interface__) and an RCCL ("nccl") sum-reduce in a world-size-1 group."""
+    import socket
+
+    import torch
+    import torch.distributed as dist
+
+    from gpu_bidirectional_raytracer_amd import sharding as shd
+
+    r, _, _ = make("cornell", 40, 24, gpu)
+    sid, vlp = schedule(3)
+    r.path_passes(sid, vlp)
+    col, cnt = r.read_radiance()
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(gpu)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", gpu))
+    try:
+        t_col, t_cnt = shd.device_tensors(r, f"cuda:{gpu}")
+        assert np.array_equal(t_col.cpu().numpy().reshape(col.shape), col)
+        assert np.array_equal(t_cnt.cpu().numpy().reshape(cnt.shape), cnt.astype(np.int32))
+        shd.reduce_frame(t_col, t_cnt)
+        torch.cuda.synchronize()
+        col2, cnt2 = r.read_radiance()               # the reduce wrote into libbdpt's buffers
+        assert_same(col2, col, "reduced colors")
+        assert_same(cnt2, cnt, "reduced counters")
+        r.update_pixels()
+    finally:
+        dist.destroy_process_group()
+        r.close()

@@ -1,0 +1,26 @@
+"""bench.py's per-sample work constants (roofline numerators) match what the oracle counts on
+the benchmark frame (cornell 1921x1081, the first pass of the reference schedule)."""
+import os
+
+import gpu_bidirectional_raytracer_amd as g
+import oracle
+from conftest import SCENES
+
+import bench
+
+
+def test_cornell_work_constants():
+    W, H = 1921, 1081
+    cam, sp = g.read_scene(os.path.join(SCENES, "cornell.scn"))
+    g.update_camera(cam, W, H)
+    rnd = oracle.mt607(0)
+    lp = oracle.light_pass(sp, rnd, 0)
+    s = g.PassScheduler()
+    s.light()
+    sid, vlp = s.next(1)
+    _, _, _, st = oracle.path_passes(sp, rnd, cam, W, H, lp, sid, vlp, stats=True)
+    n = st["samples"]
+    assert n == W * H
+    for k, v in bench.WORK["cornell"].items():
+        assert abs(st[k] / n - v) / v < 0.01, (k, st[k] / n, v)
+    assert 3400 < bench.flop_per_sample(bench.WORK["cornell"]) < 3700
