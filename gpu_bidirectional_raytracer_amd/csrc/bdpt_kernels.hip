@@ -81,7 +81,7 @@ __device__ __forceinline__ float sphere_isect_inf(float4 g, f3 o, f3 d) {
 __device__ __forceinline__ f3 uniform_sphere(float u1, float u2) {
     const float zz = 1.f - 2.f * u1;
     const float q = 1.f - zz * zz;
-    const float r = bdpt_sqrt_rn(0.f > q ? 0.f : q);
+    const float r = bdpt_sqrt_rn_core(0.f > q ? 0.f : q);   // q is 0 or >= 2^-24: core is exact
     const float phi = 2.f * kPi * u2;
     float s, c;
     sincos_cr(phi, &s, &c);
@@ -92,16 +92,17 @@ __device__ __forceinline__ f3 uniform_sphere(float u1, float u2) {
 __device__ __forceinline__ f3 cosine_dir(f3 w, float u_phi, float u_r2) {
     const float r1 = 2.f * kPi * u_phi;
     const float r2 = u_r2;
-    const float r2s = bdpt_sqrt_rn(r2);
+    const float r2s = bdpt_sqrt_rn_core(r2);                 // r2 = d_Rand value >= 2^-32
     f3 a = fabsf(w.x) > .1f ? mk(0.f, 1.f, 0.f) : mk(1.f, 0.f, 0.f);
-    f3 u = norm(cross(a, w));
+    const f3 uc = cross(a, w);                                // |uc|^2 >= 0.01 by the choice of a
+    f3 u = smul(1.f / bdpt_sqrt_rn_core(dot(uc, uc)), uc);
     f3 v = cross(w, u);
     float s, c;
     sincos_cr(r1, &s, &c);
     u = smul(c * r2s, u);
     v = smul(s * r2s, v);
     f3 nd = add(u, v);
-    w = smul(bdpt_sqrt_rn(1 - r2), w);
+    w = smul(bdpt_sqrt_rn_core(1 - r2), w);                   // 1 - r2 is 0 or >= 2^-24
     return add(nd, w);
 }
 
@@ -312,9 +313,6 @@ __global__ __launch_bounds__(256, BDPT_WAVES_PER_SIMD) void bdpt_path_kernel_t(b
         cnt = a.counter[i];
     }
     const unsigned cnt0 = cnt;
-    const float4 k4 = K[4];
-    const double kx0 = (double)((float)x * k4.x) - a.half_w;   // device.cu:565-566
-    const double ky0 = (double)((float)y * k4.y) - a.half_h;
 
     int p = 0;
     unsigned depth = 0, sid = SID[0];
@@ -328,9 +326,10 @@ __global__ __launch_bounds__(256, BDPT_WAVES_PER_SIMD) void bdpt_path_kernel_t(b
         bool done = false, diff = false;
         if (alive) {
             if (fresh) {                  // camera ray (:562-600); d_Rand[kk] == q0 (kk == j)
-                const float4 c0 = K[0], c1 = K[1], c2 = K[2], c3 = K[3];
-                const float kx = (float)(kx0 + (double)(q0 * k4.x));
-                const float ky = (float)(ky0 + (double)(q1 * k4.y));
+                const float4 c0 = K[0], c1 = K[1], c2 = K[2], c3 = K[3], k4 = K[4];
+                // device.cu:565-566: ((float)x*iw - iw*W/2.) + d_Rand[kk]*iw in fp64, then fp32
+                const float kx = (float)(((double)((float)x * k4.x) - a.half_w) + (double)(q0 * k4.x));
+                const float ky = (float)(((double)((float)y * k4.y) - a.half_h) + (double)(q1 * k4.y));
                 const float kz = 10.0f;
                 f3 rdir = mk(0.f, 0.f, 0.f);
                 rdir = add(rdir, smul(kx, mk(c0.x, c0.y, c0.z)));
@@ -394,7 +393,8 @@ __global__ __launch_bounds__(256, BDPT_WAVES_PER_SIMD) void bdpt_path_kernel_t(b
                         thr = mul(thr, mk(cm.x, cm.y, cm.z));
                         rd = refl;
                     } else {
-                        const float kq = (float)(into ? 1 : -1) * (ddn * nnt + bdpt_sqrt_rn(cos2t));
+                        // cos2t = 1 - X is 0 or >= 2^-24 (Sterbenz for X >= 1/2, else > 1/2)
+                        const float kq = (float)(into ? 1 : -1) * (ddn * nnt + bdpt_sqrt_rn_core(cos2t));
                         const f3 td = norm(sub(smul(nnt, rd), smul(kq, normal)));
                         const float aa = nt - nc, bb = nt + nc;
                         const float R0 = aa * aa / (bb * bb);
