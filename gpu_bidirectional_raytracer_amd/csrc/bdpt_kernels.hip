@@ -237,6 +237,19 @@ __device__ __forceinline__ int lane_prefix(unsigned long long mask) {
     return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32),
                                           __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
 }
+// Read-only scene data through the constant address space: wave-uniform indices become scalar
+// loads (s_load, scalar cache) that never wait on the vector-memory counter, so the in-flight RNG
+// prefetch is not drained by the traversal loops (a plain global load here costs a vmcnt(0)).
+__device__ __forceinline__ float4 ld_const(const float4* p, int i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef __attribute__((address_space(4))) const float cfloat;
+    const cfloat* q = (const cfloat*)(p + i);
+    return make_float4(q[0], q[1], q[2], q[3]);
+#else
+    return p[i];
+#endif
+}
+
 __device__ __forceinline__ void wave_lds_fence() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -285,7 +298,7 @@ __global__ __launch_bounds__(256, BDPT_WAVES_PER_SIMD) void bdpt_path_kernel_t(b
     __syncthreads();
 
     auto geom = [&](int s) -> float4 {
-        if constexpr (N > 0) return a.geom[s]; else return G[s];
+        if constexpr (N > 0) return ld_const(a.geom, s); else return G[s];
     };
     auto emissive = [&](int s) -> bool {
         if constexpr (N > 0) return (a.emis_mask >> s) & 1u;
@@ -428,8 +441,8 @@ __global__ __launch_bounds__(256, BDPT_WAVES_PER_SIMD) void bdpt_path_kernel_t(b
                 f3 sd = res, con = res;
                 float maxt = 0.f, vmaxt = 0.f;
                 if (diff && a.n_lights > 0) {
-                    const float4 lg = a.lightrec[2 * li];                 // {p, rad}
-                    const float4 le = a.lightrec[2 * li + 1];             // {e, 4*pi*rad*rad}
+                    const float4 lg = ld_const(a.lightrec, 2 * li);       // {p, rad}
+                    const float4 le = ld_const(a.lightrec, 2 * li + 1);   // {e, 4*pi*rad*rad}
                     const f3 spt = add(smul(lg.w, usp), mk(lg.x, lg.y, lg.z));
                     sd = sub(spt, ro);
                     const float len = bdpt_sqrt_rn(dot(sd, sd));

@@ -41,10 +41,10 @@ for s in $STEPS; do
     rocprofv3 -L > gpurun_out/counters_list.txt 2>&1 || true
     i=0
     for set in "${PMC_SETS[@]}"; do
-      i=$((i+1)); rm -rf gpurun_out/pmc$i
-      timeout -k 10 300 rocprofv3 --pmc $set --kernel-trace -d gpurun_out/pmc$i -o run --output-format csv -- \
-          python3 bench.py --no-cpu-baseline --steps 4 --warmup 1 ${BENCH_ARGS:-} > gpurun_out/pmc$i.log 2>&1
-      rc=$?; echo "pmc set $i ($set): rc=$rc"; tail -2 gpurun_out/pmc$i.log; ok_or_stop $rc pmc$i
+      i=$((i+1)); P=gpurun_out/${PMC_OUT:-pmc}; rm -rf $P$i; mkdir -p $(dirname $P)
+      timeout -k 10 300 rocprofv3 --pmc $set --kernel-trace -d $P$i -o run --output-format csv -- \
+          python3 bench.py --no-cpu-baseline --steps 4 --warmup 1 ${BENCH_ARGS:-} > $P$i.log 2>&1
+      rc=$?; echo "pmc set $i ($set): rc=$rc"; tail -1 $P$i.log; ok_or_stop $rc pmc$i
     done ;;
   esac
 done

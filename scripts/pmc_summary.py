@@ -4,7 +4,8 @@ import collections, csv, glob, os, sys
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
 kern = sys.argv[2] if len(sys.argv) > 2 else "path_kernel"
 vals = collections.defaultdict(list)
-for f in sorted(glob.glob(os.path.join(root, "pmc*", "run_counter_collection.csv"))):
+pat = sys.argv[3] if len(sys.argv) > 3 else "pmc*"
+for f in sorted(glob.glob(os.path.join(root, pat, "run_counter_collection.csv"))):
     for r in csv.DictReader(open(f)):
         if kern in r["Kernel_Name"]:
             vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
