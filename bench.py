@@ -24,8 +24,11 @@ METRIC = "Msamples/sec (rays·bounces/s) at 1080p cornell.scn, 1/2/4/8 GPU"
 # Per-sample work of the workload, measured once by the CPU restatement over the full 1921x1081
 # cornell frame (tests/test_work_model.py keeps these honest; DESIGN.md "Roofline").
 WORK = {
-    "cornell": {"sphere_tests": 129.47, "segments": 6.844, "diffuse": 6.139, "refr": 0.453,
-                "rng_reads": 27.007},
+    "cornell": {"sphere_tests": 129.4711, "segments": 6.8441, "diffuse": 6.1386, "refr": 0.4528, "rng_reads": 27.0071},
+    "cornell_glass": {"sphere_tests": 92.9047, "segments": 6.8374, "diffuse": 4.2323, "refr": 1.02, "rng_reads": 19.9494},
+    "caustic": {"sphere_tests": 5.1332, "segments": 1.5151, "diffuse": 0.4516, "refr": 0.0638, "rng_reads": 3.8704},
+    "simple": {"sphere_tests": 8.7195, "segments": 1.5033, "diffuse": 0.5039, "refr": 0.0, "rng_reads": 4.0156},
+    "synthetic64": {"sphere_tests": 609.1571, "segments": 6.9145, "diffuse": 5.6567, "refr": 0.908, "rng_reads": 25.5348},
 }
 # FLOP model per primitive (DESIGN.md "Roofline"): sphere test 18, segment shading 28,
 # diffuse vertex (NEE to one light + VLP + new direction) 153, refraction 40, camera ray +

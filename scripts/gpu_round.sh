@@ -37,6 +37,13 @@ for s in $STEPS; do
     timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
         python3 bench.py --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/prof.log 2>&1
     rc=$?; tail -3 gpurun_out/prof.log; find gpurun_out/prof -name "*stats*" | head; ok_or_stop $rc prof ;;
+  scenes)
+    for sc in ${SCENES_LIST:-cornell cornell_glass caustic simple synthetic64}; do
+      timeout -k 10 300 python bench.py --no-cpu-baseline --scene $sc ${BENCH_ARGS:-} > gpurun_out/scene_$sc.log 2>&1
+      rc=$?; echo "scene $sc rc=$rc $(tail -1 gpurun_out/scene_$sc.log | cut -c1-90)"
+      python -c "import json; d=json.loads(open('gpurun_out/scene_$sc.log').read().strip().splitlines()[-1]); print('   ', d['value'], 'Msamples/s', d['device_ms_per_step'], 'ms/step', 'valu', d['valu']['achieved'] if d['valu'] else None)" || true
+      ok_or_stop $rc scene_$sc
+    done ;;
   pmc)
     rocprofv3 -L > gpurun_out/counters_list.txt 2>&1 || true
     i=0

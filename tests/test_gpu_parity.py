@@ -69,7 +69,8 @@ def test_mt607_table_bit_exact(gpu, rnd0):
 
 
 @pytest.mark.parametrize("name", ["cornell", "cornell_glass", "caustic", "simple", "cornell_2luci",
-                                  "default", "cornell_multi", "hall_of_mirrors", "complex"])
+                                  "default", "cornell_multi", "hall_of_mirrors", "complex",
+                                  "synthetic64"])
 def test_light_pass_bit_exact(gpu, rnd0, name):
     r, cam, sp = make(name, 17, 9, gpu)
     ref = oracle.light_pass(sp, rnd0, 0)
@@ -98,6 +99,7 @@ def test_render_matches_golden_fixture(gpu, name):
     ("cornell_multi", 31, 23, 8), ("hall_of_mirrors", 31, 23, 8), ("gantz", 31, 23, 8),
     ("cornell_mirror_reflect", 25, 19, 8), ("complex", 17, 13, 2), ("mod_cornell", 13, 11, 2),
     ("open", 23, 17, 8), ("cornell", 1, 1, 5), ("simple", 16, 16, 3),
+    ("synthetic64", 37, 21, 6),
 ])
 def test_path_passes_bit_exact(gpu, rnd0, name, W, H, npass):
     r, cam, sp = make(name, W, H, gpu)

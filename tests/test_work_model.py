@@ -9,9 +9,13 @@ from conftest import SCENES
 import bench
 
 
-def test_cornell_work_constants():
+import pytest
+
+
+@pytest.mark.parametrize("name", sorted(bench.WORK))
+def test_work_constants(name):
     W, H = 1921, 1081
-    cam, sp = g.read_scene(os.path.join(SCENES, "cornell.scn"))
+    cam, sp = g.read_scene(os.path.join(SCENES, name + ".scn"))
     g.update_camera(cam, W, H)
     rnd = oracle.mt607(0)
     lp = oracle.light_pass(sp, rnd, 0)
@@ -21,6 +25,7 @@ def test_cornell_work_constants():
     _, _, _, st = oracle.path_passes(sp, rnd, cam, W, H, lp, sid, vlp, stats=True)
     n = st["samples"]
     assert n == W * H
-    for k, v in bench.WORK["cornell"].items():
-        assert abs(st[k] / n - v) / v < 0.01, (k, st[k] / n, v)
-    assert 3400 < bench.flop_per_sample(bench.WORK["cornell"]) < 3700
+    for k, v in bench.WORK[name].items():
+        assert abs(st[k] / n - v) <= 0.01 * abs(v) + 1e-3, (k, st[k] / n, v)
+    if name == "cornell":
+        assert 3400 < bench.flop_per_sample(bench.WORK["cornell"]) < 3700
