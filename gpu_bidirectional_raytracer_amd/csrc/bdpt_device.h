@@ -20,6 +20,15 @@
 #define BDPT_DEV_SPEC 1
 #define BDPT_DEV_REFR 2
 
+// Path-kernel tiling: a wave covers BDPT_WTW x (64/BDPT_WTW) pixels, a 256-thread workgroup 2x2
+// waves.  The host sizes the grid from the same macros.
+#ifndef BDPT_WTW
+#define BDPT_WTW 8
+#endif
+#define BDPT_WTH (64 / BDPT_WTW)
+#define BDPT_BTW (2 * BDPT_WTW)
+#define BDPT_BTH (2 * BDPT_WTH)
+
 struct bdpt_dev_vec { float x, y, z; };
 struct bdpt_dev_lightpath { float hx, hy, hz, rx, ry, rz, nx, ny, nz; };
 struct bdpt_dev_sphere {

@@ -348,7 +348,7 @@ int bdpt_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int npass
     a.orig[0] = cam.orig.x; a.orig[1] = cam.orig.y; a.orig[2] = cam.orig.z;
     a.shard = c->shard; a.nshards = c->nshards; a.band_rows = c->band_rows;
 
-    dim3 grid((c->W + 15) / 16, (c->H + 15) / 16), block(256);
+    dim3 grid((c->W + BDPT_BTW - 1) / BDPT_BTW, (c->H + BDPT_BTH - 1) / BDPT_BTH), block(256);
     const void* kern = bdpt_path_kernel_table[a.n <= 16 ? a.n : 0];
     // keep single launches bounded (~2^28 samples, <= 256 passes for the LDS pass tables)
     const long per_pass = (long)c->W * c->H;
