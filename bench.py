@@ -84,7 +84,7 @@ def main():
     ap.add_argument("--width", type=int, default=1920, help="CLI width (internal = +1)")
     ap.add_argument("--height", type=int, default=1080, help="CLI height (internal = +1)")
     ap.add_argument("--passes", type=int, default=16, help="passes per step per GPU share")
-    ap.add_argument("--band-rows", type=int, default=16)
+    ap.add_argument("--band-rows", type=int, default=8)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -166,6 +166,8 @@ def main():
         if w is not None:
             samples_per_launch = own_pixels * passes_per_launch
             bytes_per_launch = own_pixels * ACCUM_BYTES_PER_PIXEL + samples_per_launch * 4 * w["rng_reads"]
+            if r.last_streams > 1:          # pass-stream radiance: 12 B written + 12 B folded
+                bytes_per_launch += samples_per_launch * 24
             achieved = bytes_per_launch / avg_launch_s / 1e9
             traffic = None
             pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
@@ -197,7 +199,8 @@ def main():
                                    f"<=7-segment eye paths + NEE + 1 VLP per diffuse vertex",
                        "scene": args.scene, "width": W, "height": H, "passes_per_step": per_step,
                        "spp_total": per_step * (args.warmup + args.steps),
-                       "parallelism": f"pixel bands x{world} ({args.band_rows}-row, interleaved)"},
+                       "parallelism": f"pixel bands x{world} ({args.band_rows}-row, interleaved)",
+                       "pass_streams": r.last_streams},
             "device_ms_per_step": round(dev_ms / args.steps, 3),
             "roofline": roofline, "valu": valu, "cpu_baseline": cpu,
         }

@@ -196,8 +196,16 @@ class Renderer:
     def reset_accum(self) -> None:
         self._chk(lib.bdpt_reset_accum(self._h))
 
-    def set_shard(self, shard: int, nshards: int, band_rows: int = 16) -> None:
+    def set_shard(self, shard: int, nshards: int, band_rows: int = 8) -> None:
         self._chk(lib.bdpt_set_shard(self._h, shard, nshards, band_rows))
+
+    def set_streams(self, streams: int) -> None:
+        """Pass streams per pixel (0 = auto); results are bit-identical for every value."""
+        self._chk(lib.bdpt_set_streams(self._h, streams))
+
+    @property
+    def last_streams(self) -> int:
+        return int(lib.bdpt_last_streams(self._h))
 
     # -- work
     def generate_rand(self, seed: int) -> None:

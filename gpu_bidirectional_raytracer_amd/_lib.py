@@ -67,6 +67,8 @@ _SIGS = [
     ("bdpt_set_camera", ctypes.c_int, [_P, ctypes.POINTER(Camera)]),
     ("bdpt_reset_accum", ctypes.c_int, [_P]),
     ("bdpt_set_shard", ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    ("bdpt_set_streams", ctypes.c_int, [_P, ctypes.c_int]),
+    ("bdpt_last_streams", ctypes.c_int, [_P]),
     ("bdpt_light_pass", ctypes.c_int, [_P, ctypes.c_int]),
     ("bdpt_generate_rand", ctypes.c_int, [_P, ctypes.c_uint]),
     ("bdpt_path_passes", ctypes.c_int, [_P, _P, _P, ctypes.c_int]),

@@ -20,14 +20,19 @@
 #define BDPT_DEV_SPEC 1
 #define BDPT_DEV_REFR 2
 
-// Path-kernel tiling: a wave covers BDPT_WTW x (64/BDPT_WTW) pixels, a 256-thread workgroup 2x2
-// waves.  The host sizes the grid from the same macros.
+// Path-kernel tiling: a wave covers BDPT_WTW x (64/BDPT_WTW) pixels, a 256-thread workgroup
+// BDPT_BLOCK_WX x (4/BDPT_BLOCK_WX) waves (default 4x1: a 32x8 tile, so 8-row shard bands map to
+// whole tile rows).  The host sizes the grid from the same macros.
 #ifndef BDPT_WTW
 #define BDPT_WTW 8
 #endif
+#ifndef BDPT_BLOCK_WX
+#define BDPT_BLOCK_WX 4
+#endif
 #define BDPT_WTH (64 / BDPT_WTW)
-#define BDPT_BTW (2 * BDPT_WTW)
-#define BDPT_BTH (2 * BDPT_WTH)
+#define BDPT_BLOCK_WY (4 / BDPT_BLOCK_WX)
+#define BDPT_BTW (BDPT_BLOCK_WX * BDPT_WTW)
+#define BDPT_BTH (BDPT_BLOCK_WY * BDPT_WTH)
 
 struct bdpt_dev_vec { float x, y, z; };
 struct bdpt_dev_lightpath { float hx, hy, hz, rx, ry, rz, nx, ny, nz; };
@@ -61,7 +66,18 @@ struct bdpt_path_args {
     float ux[3], uy[3], ud[3], orig[3];
     float tx, ty, tz;
     int shard, nshards, band_rows;
+    int tiles_per_band;             // > 0: grid rows enumerate only this shard's bands
+    int streams;                    // pass streams S: lane (pixel, s) renders passes s, s+S, ...
+    bdpt_dev_vec* rbuf;             // S > 1: per (pass, launched pixel) radiance, [npass][nloc]
+    int nloc;                       // launched pixels per pass = gridDim.y * BDPT_BTH * W
 };
+
+// Tile row of a workgroup row: identity, or the sub-th tile row of this shard's k-th band.
+__device__ __forceinline__ int bdpt_dev_tile_row(const bdpt_path_args& a, int by) {
+    if (a.tiles_per_band <= 0) return by;
+    const int k = by / a.tiles_per_band, sub = by - k * a.tiles_per_band;
+    return (a.shard + k * a.nshards) * a.tiles_per_band + sub;
+}
 
 // toInt (vec.h:34) by threshold search: thr[k] is the smallest float whose toInt is >= k,
 // computed on the host with the same pow as the reference semantics; 8 compares per channel.

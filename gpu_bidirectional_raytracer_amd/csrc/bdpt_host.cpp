@@ -27,8 +27,9 @@ static_assert(sizeof(bdpt_dev_vec) == sizeof(bdpt_vec), "colour layout");
 extern "C" __global__ void bdpt_mt607_kernel(const uint4*, unsigned, float*);
 extern "C" __global__ void bdpt_light_kernel(const bdpt_dev_sphere*, unsigned, const float*, int,
                                              bdpt_dev_lightpath*);
-extern "C" const void* bdpt_path_kernel_table[17];   // [n] for n <= 16, [0] generic
+extern "C" const void* bdpt_path_kernel_table[34];   // [(S > 1) * 17 + (n <= 16 ? n : 0)]
 extern "C" __global__ void bdpt_pixels_kernel(const bdpt_dev_vec*, uchar4*, const float*, int);
+extern "C" __global__ void bdpt_accum_kernel(bdpt_path_args);
 
 // gamma thresholds (host, once): see bdpt_util.c
 extern "C" void bdpt_gamma_thresholds(float thr[256]);
@@ -48,7 +49,12 @@ struct bdpt_ctx {
     bdpt_camera cam{};
     bool cam_set = false;
     bool rand_ready = false;
-    int shard = 0, nshards = 1, band_rows = 16;
+    int shard = 0, nshards = 1, band_rows = 8;
+    int streams_req = 0;                // bdpt_set_streams: 0 = auto
+    int last_streams = 1;               // S of the last path-pass launch
+    int cus = 256;                      // compute units (auto stream count)
+    bdpt_dev_vec* d_rbuf = nullptr;     // pass-stream radiance, [npass][nloc]
+    size_t rbuf_cap = 0;                // elements
     uint4* d_params = nullptr;          // 4096 x {matrix_a, mask_b, mask_c, seed}
     float* d_rand = nullptr;
     bdpt_dev_lightpath* d_lp = nullptr;
@@ -136,7 +142,7 @@ static int upload_scene(bdpt_ctx* c) {
 
 static void release(bdpt_ctx* c) {
     void* bufs[] = {c->d_params, c->d_rand, c->d_lp, c->d_sph, c->d_lights, c->d_geom, c->d_lightrec, c->d_colors,
-                    c->d_counter, c->d_pixels, c->d_thr, c->d_sid, c->d_vlp};
+                    c->d_counter, c->d_pixels, c->d_thr, c->d_sid, c->d_vlp, c->d_rbuf};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -191,6 +197,11 @@ int bdpt_create(bdpt_ctx** out, const bdpt_sphere* spheres, unsigned n, int W, i
         fail(c, BDPT_EHIP, "%s: %s", #call, hipGetErrorString(e_)); return bail(BDPT_EHIP); } } while (0)
     CK(hipSetDevice(device));
     CK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
+            c->cus = cus;
+    }
     CK(hipEventCreate(&c->ev0));
     CK(hipEventCreate(&c->ev1));
     const size_t np = (size_t)W * H;
@@ -254,6 +265,16 @@ int bdpt_set_shard(bdpt_ctx* c, int shard, int nshards, int band_rows) {
     c->shard = shard; c->nshards = nshards; c->band_rows = band_rows;
     return BDPT_OK;
 }
+
+int bdpt_set_streams(bdpt_ctx* c, int streams) {
+    if (!c) return BDPT_EINVAL;
+    if (streams < 0 || streams > BDPT_MAX_STREAMS)
+        return fail(c, BDPT_EINVAL, "bdpt_set_streams: bad stream count %d", streams);
+    c->streams_req = streams;
+    return BDPT_OK;
+}
+
+int bdpt_last_streams(const bdpt_ctx* c) { return c ? c->last_streams : BDPT_EINVAL; }
 
 int bdpt_generate_rand(bdpt_ctx* c, unsigned seed) {
     if (!c) return BDPT_EINVAL;
@@ -348,16 +369,55 @@ int bdpt_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int npass
     a.orig[0] = cam.orig.x; a.orig[1] = cam.orig.y; a.orig[2] = cam.orig.z;
     a.shard = c->shard; a.nshards = c->nshards; a.band_rows = c->band_rows;
 
-    dim3 grid((c->W + BDPT_BTW - 1) / BDPT_BTW, (c->H + BDPT_BTH - 1) / BDPT_BTH), block(256);
-    const void* kern = bdpt_path_kernel_table[a.n <= 16 ? a.n : 0];
-    // keep single launches bounded (~2^28 samples, <= 256 passes for the LDS pass tables)
-    const long per_pass = (long)c->W * c->H;
-    int chunk = (int)((1L << 28) / (per_pass > 0 ? per_pass : 1));
+    // Grid rows: every tile row, or (bands a whole number of tile rows) only this shard's bands.
+    const int tile_rows = (c->H + BDPT_BTH - 1) / BDPT_BTH;
+    int grid_rows = tile_rows;
+    a.tiles_per_band = 0;
+    if (c->nshards > 1 && c->band_rows % BDPT_BTH == 0) {
+        const int tpb = c->band_rows / BDPT_BTH;
+        const int nbands = (c->H + c->band_rows - 1) / c->band_rows;
+        const int owned = c->shard < nbands ? (nbands - c->shard + c->nshards - 1) / c->nshards : 0;
+        a.tiles_per_band = tpb;
+        grid_rows = owned * tpb;
+    }
+    // Pass streams: enough lanes for ~3 rounds of 5 waves per SIMD (a shard of a multi-GPU
+    // frame, or a small image, has fewer pixels than that), else 1.
+    const long lanes = (long)grid_rows * BDPT_BTH * c->W;
+    int S = c->streams_req;
+    if (S == 0) {
+        const long target = 3L * 5 * 4 * c->cus * 64;
+        S = lanes > 0 ? (int)((target + lanes - 1) / lanes) : 1;
+        if (S > 16) S = 16;
+    }
+    a.nloc = (int)lanes;
+    dim3 grid((c->W + BDPT_BTW - 1) / BDPT_BTW, grid_rows, 1), block(256);
+    // keep single launches bounded (~2^28 samples, <= 128 passes for the LDS pass tables)
+    const long per_pass = lanes > 0 ? lanes : 1;
+    int chunk = (int)((1L << 28) / per_pass);
     if (chunk < 1) chunk = 1;
     if (chunk > 128) chunk = 128;
+    if (S > chunk) S = chunk;
+    if (S > npass) S = npass;
+    if (S < 1) S = 1;
+    a.streams = S;
+    c->last_streams = S;
+    const void* kern = bdpt_path_kernel_table[(S > 1) * 17 + (a.n <= 16 ? a.n : 0)];
+    if (S > 1) {
+        const int cmax = npass < chunk ? npass : chunk;
+        const size_t need = (size_t)cmax * (size_t)lanes;
+        if (need > c->rbuf_cap) {
+            if (c->d_rbuf) HIPCHK(c, hipFree(c->d_rbuf));
+            c->d_rbuf = nullptr;
+            c->rbuf_cap = 0;
+            if (hipMalloc(&c->d_rbuf, sizeof(bdpt_dev_vec) * need) != hipSuccess)
+                return fail(c, BDPT_ENOMEM, "bdpt_path_passes: pass-stream buffer (%zu B)", sizeof(bdpt_dev_vec) * need);
+            c->rbuf_cap = need;
+        }
+        a.rbuf = c->d_rbuf;
+    }
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     int launches = 0;
-    for (int p0 = 0; p0 < npass; p0 += chunk, launches++) {
+    for (int p0 = 0; grid_rows > 0 && p0 < npass; p0 += chunk, launches++) {
         a.sid = c->d_sid + p0;
         a.vlp = c->d_vlp + p0;
         a.npass = npass - p0 < chunk ? npass - p0 : chunk;
@@ -367,7 +427,12 @@ int bdpt_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int npass
         if (smem > 160 * 1024)
             return fail(c, BDPT_EINVAL, "bdpt_path_passes: scene too large for LDS (%u spheres)", a.n);
         void* kargs[] = {&a};
+        grid.z = S;
         HIPCHK(c, hipLaunchKernel(kern, grid, block, kargs, smem, c->stream));
+        if (S > 1) {
+            grid.z = 1;
+            HIPCHK(c, hipLaunchKernel((const void*)&bdpt_accum_kernel, grid, block, kargs, 0, c->stream));
+        }
     }
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
     c->timed = true;

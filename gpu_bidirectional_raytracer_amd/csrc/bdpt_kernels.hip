@@ -228,7 +228,8 @@ extern "C" __global__ __launch_bounds__(64) void bdpt_light_kernel(const bdpt_de
 //    VLP (dev_lp[vlp_index]) and the camera constants are LDS tables.
 //  * The 5 random numbers a segment may consume (d_Rand[j..j+4], j = (26+25i+5*depth+sid) mod
 //    (RAND_N-5), device.cu:619) are prefetched one segment ahead.
-//  * 256-thread workgroup = 16x16 pixel tile as 2x2 waves of 8x8 pixels.
+//  * 256-thread workgroup = 32x8 pixel tile as 4x1 waves of 8x8 pixels; blockIdx.z = pass
+//    stream when the launch has fewer pixels than the chip has lanes (multi-GPU shards).
 // =============================================================================================
 namespace {
 constexpr int kQueue = 128;                       // shadow rays per wave and step (<= 2 per lane)
@@ -259,7 +260,7 @@ __device__ __forceinline__ void wave_lds_fence() {
 #ifndef BDPT_WAVES_PER_SIMD
 #define BDPT_WAVES_PER_SIMD 5
 #endif
-template <int N>
+template <int N, bool STREAMS>
 __global__ __launch_bounds__(256, BDPT_WAVES_PER_SIMD) void bdpt_path_kernel_t(bdpt_path_args a) {
     extern __shared__ float4 smem[];
     const int n = N > 0 ? N : (int)a.n;
@@ -306,10 +307,16 @@ __global__ __launch_bounds__(256, BDPT_WAVES_PER_SIMD) void bdpt_path_kernel_t(b
     };
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int x = blockIdx.x * BDPT_BTW + (wave & 1) * BDPT_WTW + (lane % BDPT_WTW);
-    const int y = blockIdx.y * BDPT_BTH + (wave >> 1) * BDPT_WTH + (lane / BDPT_WTW);
+    const int x = blockIdx.x * BDPT_BTW + (wave % BDPT_BLOCK_WX) * BDPT_WTW + (lane % BDPT_WTW);
+    const int ly = blockIdx.y * BDPT_BTH + (wave / BDPT_BLOCK_WX) * BDPT_WTH + (lane / BDPT_WTW);
+    const int yoff = (bdpt_dev_tile_row(a, blockIdx.y) - (int)blockIdx.y) * BDPT_BTH;   // uniform
+    const int y = ly + yoff;
     bool active = x < a.W && y < a.H;
     if (active && a.nshards > 1) active = ((y / a.band_rows) % a.nshards) == a.shard;
+    // pass stream: this lane renders passes s, s+S, s+2S, ... of its pixel (S == 1: all, and
+    // it keeps the running mean itself; S > 1: radiance goes to rbuf, bdpt_accum_kernel folds
+    // it in pass order).  Pass p is rendered iff counter0 + p < 30000 (one increment per pass).
+    const int S = STREAMS ? a.streams : 1, s0 = STREAMS ? (int)blockIdx.z : 0;
     float4* SQ = Q + wave * kQueue * 2;
     unsigned* SR = R + wave * kQueue;
 
@@ -319,21 +326,22 @@ __global__ __launch_bounds__(256, BDPT_WAVES_PER_SIMD) void bdpt_path_kernel_t(b
     constexpr unsigned M5 = kRandN - 5u;
 
     f3 col = mk(0.f, 0.f, 0.f);
-    unsigned cnt = 0;
+    unsigned cnt0 = 0;                // the counter before pass p is cnt0 + p
     if (active) {
-        const bdpt_dev_vec cv = a.colors[i];
-        col = mk(cv.x, cv.y, cv.z);
-        cnt = a.counter[i];
+        if constexpr (!STREAMS) {
+            const bdpt_dev_vec cv = a.colors[i];
+            col = mk(cv.x, cv.y, cv.z);
+        }
+        cnt0 = a.counter[i];
     }
-    const unsigned cnt0 = cnt;
 
-    int p = 0;
-    unsigned depth = 0, sid = SID[0];
+    int p = s0;
+    unsigned depth = 0, sid = SID[p < a.npass ? p : 0];
     unsigned j = (ibase + sid) % M5;
     float q0 = rnd[j], q1 = rnd[j + 1], q2 = rnd[j + 2], q3 = rnd[j + 3], q4 = rnd[j + 4];
     f3 ro = mk(0.f, 0.f, 0.f), rd = ro, thr = ro, rad = ro, nl = ro;
     bool specular = true, fresh = true;
-    bool alive = active && p < a.npass && cnt < BDPT_DEV_COUNTER_CAP;
+    bool alive = active && p < a.npass && cnt0 + (unsigned)p < BDPT_DEV_COUNTER_CAP;
 
     while (__builtin_amdgcn_ballot_w64(alive) != 0) {                   // wave-uniform loop
         bool done = false, diff = false;
@@ -528,20 +536,26 @@ __global__ __launch_bounds__(256, BDPT_WAVES_PER_SIMD) void bdpt_path_kernel_t(b
         if (alive) {
             if (!done && ++depth > 6) done = true;                       // :621 7-segment cap
             if (done) {                                                  // :774-787
-                if (cnt == 0) {
-                    col = rad;
+                if constexpr (!STREAMS) {
+                    const unsigned cnt = cnt0 + (unsigned)p;
+                    if (cnt == 0) {
+                        col = rad;
+                    } else {
+                        const float k1 = (float)cnt;
+                        const float k2 = 1.f / (k1 + 1.f);
+                        col.x = (col.x * k1 + rad.x) * k2;
+                        col.y = (col.y * k1 + rad.y) * k2;
+                        col.z = (col.z * k1 + rad.z) * k2;
+                    }
                 } else {
-                    const float k1 = (float)cnt;
-                    const float k2 = 1.f / (k1 + 1.f);
-                    col.x = (col.x * k1 + rad.x) * k2;
-                    col.y = (col.y * k1 + rad.y) * k2;
-                    col.z = (col.z * k1 + rad.z) * k2;
+                    bdpt_dev_vec r;
+                    r.x = rad.x; r.y = rad.y; r.z = rad.z;
+                    a.rbuf[(size_t)p * a.nloc + (size_t)(i - yoff * a.W)] = r;
                 }
-                cnt++;
-                p++;
+                p += S;
                 fresh = true;
                 depth = 0;
-                alive = p < a.npass && cnt < BDPT_DEV_COUNTER_CAP;
+                alive = p < a.npass && cnt0 + (unsigned)p < BDPT_DEV_COUNTER_CAP;
                 if (alive) sid = SID[p];
             }
             if (alive) {                  // prefetch the next segment's random numbers (:619)
@@ -550,7 +564,8 @@ __global__ __launch_bounds__(256, BDPT_WAVES_PER_SIMD) void bdpt_path_kernel_t(b
             }
         }
     }
-    if (!active || cnt == cnt0) return;                                  // nothing rendered
+    if (STREAMS || !active || p == s0) return;                           // nothing rendered
+    const unsigned cnt = cnt0 + (unsigned)p;
     bdpt_dev_vec out;
     out.x = col.x; out.y = col.y; out.z = col.z;
     a.colors[i] = out;
@@ -558,23 +573,48 @@ __global__ __launch_bounds__(256, BDPT_WAVES_PER_SIMD) void bdpt_path_kernel_t(b
     a.pixels[i] = bdpt_dev_to_rgba(col.x, col.y, col.z, a.gamma_thr);
 }
 
-#define BDPT_INST(NN) template __global__ void bdpt_path_kernel_t<NN>(bdpt_path_args);
-BDPT_INST(0) BDPT_INST(1) BDPT_INST(2) BDPT_INST(3) BDPT_INST(4) BDPT_INST(5) BDPT_INST(6)
-BDPT_INST(7) BDPT_INST(8) BDPT_INST(9) BDPT_INST(10) BDPT_INST(11) BDPT_INST(12)
-BDPT_INST(13) BDPT_INST(14) BDPT_INST(15) BDPT_INST(16)
-#undef BDPT_INST
+// host-side launch table: [streams * 17 + sphere count], count 0 = generic LDS traversal
+#define BDPT_K(NN, ST) (const void*)&bdpt_path_kernel_t<NN, ST>
+#define BDPT_ROW(ST) BDPT_K(0, ST), BDPT_K(1, ST), BDPT_K(2, ST), BDPT_K(3, ST), BDPT_K(4, ST), \
+    BDPT_K(5, ST), BDPT_K(6, ST), BDPT_K(7, ST), BDPT_K(8, ST), BDPT_K(9, ST), BDPT_K(10, ST), \
+    BDPT_K(11, ST), BDPT_K(12, ST), BDPT_K(13, ST), BDPT_K(14, ST), BDPT_K(15, ST), BDPT_K(16, ST)
+extern "C" const void* bdpt_path_kernel_table[34] = {BDPT_ROW(false), BDPT_ROW(true)};
+#undef BDPT_ROW
+#undef BDPT_K
 
-// host-side launch table (index = sphere count, 0 = generic LDS traversal)
-extern "C" const void* bdpt_path_kernel_table[17] = {
-    (const void*)&bdpt_path_kernel_t<0>, (const void*)&bdpt_path_kernel_t<1>,
-    (const void*)&bdpt_path_kernel_t<2>, (const void*)&bdpt_path_kernel_t<3>,
-    (const void*)&bdpt_path_kernel_t<4>, (const void*)&bdpt_path_kernel_t<5>,
-    (const void*)&bdpt_path_kernel_t<6>, (const void*)&bdpt_path_kernel_t<7>,
-    (const void*)&bdpt_path_kernel_t<8>, (const void*)&bdpt_path_kernel_t<9>,
-    (const void*)&bdpt_path_kernel_t<10>, (const void*)&bdpt_path_kernel_t<11>,
-    (const void*)&bdpt_path_kernel_t<12>, (const void*)&bdpt_path_kernel_t<13>,
-    (const void*)&bdpt_path_kernel_t<14>, (const void*)&bdpt_path_kernel_t<15>,
-    (const void*)&bdpt_path_kernel_t<16>};
+// Ordered fold of pass-stream radiance (S > 1): the running mean of device.cu:774-787 applied
+// to rbuf[0..npass) in pass order, so the result is the S == 1 result bit for bit.  Same grid
+// rows (and shard remap) as the path launch; one thread per pixel.
+extern "C" __global__ __launch_bounds__(256) void bdpt_accum_kernel(bdpt_path_args a) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int x = blockIdx.x * BDPT_BTW + (wave % BDPT_BLOCK_WX) * BDPT_WTW + (lane % BDPT_WTW);
+    const int ly = blockIdx.y * BDPT_BTH + (wave / BDPT_BLOCK_WX) * BDPT_WTH + (lane / BDPT_WTW);
+    const int y = bdpt_dev_tile_row(a, blockIdx.y) * BDPT_BTH + (ly - blockIdx.y * BDPT_BTH);
+    if (x >= a.W || y >= a.H) return;
+    if (a.nshards > 1 && ((y / a.band_rows) % a.nshards) != a.shard) return;
+    const int i = y * a.W + x;
+    const size_t li = (size_t)ly * a.W + x;
+    const unsigned cnt0 = a.counter[i];
+    unsigned cnt = cnt0;
+    bdpt_dev_vec col = a.colors[i];
+    for (int p = 0; p < a.npass && cnt < BDPT_DEV_COUNTER_CAP; p++) {
+        const bdpt_dev_vec r = a.rbuf[(size_t)p * a.nloc + li];
+        if (cnt == 0) {
+            col = r;
+        } else {
+            const float k1 = (float)cnt;
+            const float k2 = 1.f / (k1 + 1.f);
+            col.x = (col.x * k1 + r.x) * k2;
+            col.y = (col.y * k1 + r.y) * k2;
+            col.z = (col.z * k1 + r.z) * k2;
+        }
+        cnt++;
+    }
+    if (cnt == cnt0) return;
+    a.colors[i] = col;
+    a.counter[i] = cnt;
+    a.pixels[i] = bdpt_dev_to_rgba(col.x, col.y, col.z, a.gamma_thr);
+}
 
 // Recompute pixels from colors (after a cross-GPU reduce of the radiance frame).
 extern "C" __global__ __launch_bounds__(256) void bdpt_pixels_kernel(const bdpt_dev_vec* __restrict__ colors,

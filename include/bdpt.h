@@ -36,6 +36,7 @@ typedef struct { bdpt_vec orig, target, dir, x, y; } bdpt_camera;
 #define BDPT_LIGHT_POINTS 4096              /* geom.h:15 LIGHT_POINTS (DEPTH=1, MAX_VLP=1)  */
 #define BDPT_MAX_SEGMENTS 7                 /* device.cu:621 `depth > 6` break               */
 #define BDPT_COUNTER_CAP  30000u            /* device.cu:607 `counter[i] < 30000`            */
+#define BDPT_MAX_STREAMS  128               /* bdpt_set_streams upper bound                  */
 
 /* Error codes. */
 #define BDPT_OK        0
@@ -69,8 +70,16 @@ int  bdpt_set_camera(bdpt_ctx *ctx, const bdpt_camera *camera);
  * next pass because counter==0 assigns (device.cu:774). */
 int  bdpt_reset_accum(bdpt_ctx *ctx);
 /* Multi-GPU sharding: only pixels whose row band (y / band_rows) % nshards == shard are
- * rendered; all other pixels stay zero so a sum-reduce of the frames is exact. Default 0,1,*. */
+ * rendered; all other pixels stay zero so a sum-reduce of the frames is exact. Default 0,1,8;
+ * band_rows a multiple of 8 (the tile height) launches only the shard's own tile rows. */
 int  bdpt_set_shard(bdpt_ctx *ctx, int shard, int nshards, int band_rows);
+/* Pass streams (no reference counterpart; results are bit-identical for every S): S lanes per
+ * pixel render passes s, s+S, ... into an HBM radiance buffer and an ordered fold applies the
+ * running mean of device.cu:774-787 in pass order.  0 = auto (S > 1 only when the launch has
+ * fewer pixels than ~3 rounds of resident waves, e.g. a multi-GPU shard), else 1..128. */
+int  bdpt_set_streams(bdpt_ctx *ctx, int streams);
+/* S used by the last bdpt_path_passes call. */
+int  bdpt_last_streams(const bdpt_ctx *ctx);
 
 /* UpdateRendering2 smallpt_cpu.c:300-362: for every emitter in sphere order,
  * seedMTGPU(current_sample*5) + RandomGPU (MT607 table), GetRayKernel and

@@ -44,6 +44,9 @@ for s in $STEPS; do
       python -c "import json; d=json.loads(open('gpurun_out/scene_$sc.log').read().strip().splitlines()[-1]); print('   ', d['value'], 'Msamples/s', d['device_ms_per_step'], 'ms/step', 'valu', d['valu']['achieved'] if d['valu'] else None)" || true
       ok_or_stop $rc scene_$sc
     done ;;
+  shard)
+    timeout -k 10 400 python scripts/shard_probe.py ${SHARD_ARGS:-} > gpurun_out/shard_probe.log 2>&1
+    rc=$?; cat gpurun_out/shard_probe.log | tail -12; ok_or_stop $rc shard ;;
   pmc)
     rocprofv3 -L > gpurun_out/counters_list.txt 2>&1 || true
     i=0

@@ -1,0 +1,69 @@
+"""Single-GPU rehearsal of the multi-GPU weak-scaling step (bench.py --gpus N).
+
+For each N, rank 0's share of an N-way band shard (1/N of the rows, N x passes) is rendered on
+one GPU with auto pass streams and with S = 1, and its device time is compared with the N = 1
+step; efficiency = t(N=1) / t(rank share).  The RCCL reduce is not included (it runs once per
+frame, not per step).
+
+    python scripts/shard_probe.py [--scene cornell] [--passes 16] [--reps 3]
+"""
+import argparse
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+import gpu_bidirectional_raytracer_amd as g  # noqa: E402
+
+
+def run(sp, cam, W, H, sid, vlp, shard, nshards, band, streams, reps):
+    r = g.Renderer(sp, W, H, cam, device=0)
+    r.set_shard(shard, nshards, band)
+    r.set_streams(streams)
+    r.light_pass(0)
+    n = len(sid) // (reps + 1)
+    r.path_passes(sid[:n], vlp[:n])                     # warmup
+    r.synchronize()
+    r.path_timing(reset=True)
+    for k in range(1, reps + 1):
+        r.path_passes(sid[k * n:(k + 1) * n], vlp[k * n:(k + 1) * n])
+    r.synchronize()
+    ms, launches = r.path_timing()
+    S = r.last_streams
+    r.close()
+    return ms / reps, S
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scene", default="cornell")
+    ap.add_argument("--passes", type=int, default=16)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--band-rows", type=int, default=8)
+    ap.add_argument("--ns", default="1,2,4,8")
+    args = ap.parse_args()
+    W, H = 1921, 1081
+    cam, sp = g.read_scene(os.path.join(REPO, "assets", "scenes", args.scene + ".scn"))
+    g.update_camera(cam, W, H)
+    sched = g.PassScheduler()
+    sched.light()
+    t1 = None
+    for N in [int(x) for x in args.ns.split(",")]:
+        sid, vlp = sched.next(args.passes * N * (args.reps + 1))
+        for streams in ([0] if N == 1 else [0, 1]):
+            worst = 0.0
+            for shard in sorted({0, N - 1}):
+                ms, S = run(sp, cam, W, H, sid, vlp, shard, N, args.band_rows, streams, args.reps)
+                worst = max(worst, ms)
+            if N == 1:
+                t1 = worst
+            print(json.dumps({"N": N, "streams_req": streams, "streams": S, "ms_per_step": round(worst, 3),
+                              "efficiency": round(t1 / worst, 4),
+                              "whole_job_Msamples_s": round(W * H * args.passes * N / worst / 1e3, 1)}),
+                  flush=True)
+
+
+if __name__ == "__main__":
+    main()

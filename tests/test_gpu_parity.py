@@ -127,18 +127,23 @@ def test_split_launches_equal_one_launch(gpu):
     a.close(); b.close()
 
 
-def test_shards_sum_to_full_frame(gpu):
+@pytest.mark.parametrize("band,streams", [(16, 0), (8, 0), (8, 1), (5, 0), (24, 3)])
+def test_shards_sum_to_full_frame(gpu, band, streams):
+    """Bands that are whole tile rows launch only the shard's tiles (remapped grid rows); other
+    band heights fall back to a per-pixel ownership test.  Either way the sum is the frame."""
     sid, vlp = schedule(4)
     full, _, _ = make("cornell_glass", 45, 70, gpu)
+    full.set_streams(1)
     full.path_passes(sid, vlp)
     fc, fn = full.read_radiance()
     acc_c, acc_n = np.zeros_like(fc), np.zeros_like(fn)
     for s in range(3):
         r, _, _ = make("cornell_glass", 45, 70, gpu)
-        r.set_shard(s, 3, 16)
+        r.set_shard(s, 3, band)
+        r.set_streams(streams)
         r.path_passes(sid, vlp)
         c, n = r.read_radiance()
-        owned = ((np.arange(70) // 16) % 3 == s)
+        owned = ((np.arange(70) // band) % 3 == s)
         assert (n[~owned] == 0).all() and (n[owned] == 4).all()
         acc_c += c
         acc_n += n
@@ -146,6 +151,43 @@ def test_shards_sum_to_full_frame(gpu):
     assert_same(acc_c, fc, "shard sum colors")
     assert_same(acc_n, fn, "shard sum counter")
     full.close()
+
+
+@pytest.mark.parametrize("streams", [1, 2, 3, 7, 16])
+def test_pass_streams_bit_exact(gpu, rnd0, streams):
+    """S lanes per pixel render passes s, s+S, ...; the ordered fold must give the oracle's
+    running mean bit for bit, across split calls (11 passes: S clamps to the call's count)."""
+    W, H = 37, 29
+    r, cam, sp = make("cornell_glass", W, H, gpu)
+    r.set_streams(streams)
+    sid, vlp = schedule(16)
+    r.path_passes(sid[:5], vlp[:5])
+    assert r.last_streams == min(streams, 5)
+    r.path_passes(sid[5:], vlp[5:])
+    assert r.last_streams == min(streams, 11)
+    col, cnt = r.read_radiance()
+    lp = oracle.light_pass(sp, rnd0, 0)
+    ocol, ocnt, opix = oracle.path_passes(sp, rnd0, cam, W, H, lp, sid, vlp)
+    assert_same(cnt, ocnt, "counter")
+    assert_same(col, ocol, "colors")
+    assert_same(r.read_pixels(), opix, "pixels")
+    r.close()
+
+
+def test_auto_streams_policy(gpu):
+    """Auto: S = 1 for a full 1080p frame, S > 1 for a small frame or an 8-way shard of 1080p."""
+    r, _, _ = make("cornell", 1921, 1081, gpu)
+    sid, vlp = schedule(8)
+    r.path_passes(sid[:1], vlp[:1])
+    assert r.last_streams == 1
+    r.set_shard(3, 8, 8)
+    r.path_passes(sid[:8], vlp[:8])
+    assert r.last_streams == 4
+    r.close()
+    s, _, _ = make("cornell", 65, 49, gpu)
+    s.path_passes(sid, vlp)
+    assert s.last_streams == 8
+    s.close()
 
 
 def test_reset_accum_and_scene_edit(gpu, rnd0):
@@ -168,11 +210,14 @@ def test_reset_accum_and_scene_edit(gpu, rnd0):
     r.close()
 
 
-def test_counter_cap_30000(gpu, rnd0):
+@pytest.mark.parametrize("streams", [0, 1])
+def test_counter_cap_30000(gpu, rnd0, streams):
     W, H = 3, 2
     r, cam, sp = make("simple", W, H, gpu)
+    r.set_streams(streams)
     sid, vlp = schedule(30004)
-    r.path_passes(sid, vlp)
+    r.path_passes(sid[:29990], vlp[:29990])
+    r.path_passes(sid[29990:], vlp[29990:])   # the cap falls inside this call
     col, cnt = r.read_radiance()
     assert (cnt == 30000).all()
     lp = oracle.light_pass(sp, rnd0, 0)
