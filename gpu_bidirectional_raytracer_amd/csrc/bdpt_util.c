@@ -18,7 +18,9 @@ static bdpt_vec vadd(bdpt_vec a, bdpt_vec b) { return vinit(a.x + b.x, a.y + b.y
 static bdpt_vec vsub(bdpt_vec a, bdpt_vec b) { return vinit(a.x - b.x, a.y - b.y, a.z - b.z); }
 static bdpt_vec vsmul(float k, bdpt_vec b) { return vinit(k * b.x, k * b.y, k * b.z); }
 static float vdot(bdpt_vec a, bdpt_vec b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
-static bdpt_vec vnorm(bdpt_vec v) { float l = 1.f / sqrtf(vdot(v, v)); return vsmul(l, v); }
+/* vnorm (vec.h:22) as the reference's host C code compiles it: `sqrt` of a float in C is the
+ * double libm sqrt, so l = (float)(1.f / sqrt((double)dot)) with one final rounding. */
+static bdpt_vec vnorm(bdpt_vec v) { float l = (float)(1.f / sqrt((double)vdot(v, v))); return vsmul(l, v); }
 static bdpt_vec vxcross(bdpt_vec a, bdpt_vec b) {
     return vinit(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }

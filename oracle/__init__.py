@@ -41,6 +41,10 @@ def _load():
     lib.oracle_path_passes.restype = None
     lib.oracle_update_camera.argtypes = [P, ctypes.c_int, ctypes.c_int]
     lib.oracle_update_camera.restype = None
+    lib.oracle_key_camera.argtypes = [P, ctypes.c_int]
+    lib.oracle_key_camera.restype = ctypes.c_int
+    lib.oracle_special_key.argtypes = [P, ctypes.c_int]
+    lib.oracle_special_key.restype = ctypes.c_int
     lib.oracle_to_int.argtypes = [ctypes.c_float]
     lib.oracle_to_int.restype = ctypes.c_int
     lib.oracle_fnv1a64.argtypes = [P, ctypes.c_uint64]
@@ -97,6 +101,22 @@ def update_camera(orig, target, width: int, height: int) -> np.ndarray:
     c["target"] = target
     lib.oracle_update_camera(_p(c), width, height)
     return c
+
+
+GLUT_SPECIAL = {"left": 100, "up": 101, "right": 102, "down": 103, "page_up": 104, "page_down": 105}
+
+
+def key_camera(cam: np.ndarray, key: str) -> bool:
+    """KeyFunc camera keys (display_func.c:276-336) on a CAMERA_DTYPE array, in place.
+    True when the reference calls ReInit(1) for the key."""
+    assert cam.dtype == CAMERA_DTYPE and cam.flags.c_contiguous
+    return bool(lib.oracle_key_camera(_p(cam), ord(key)))
+
+
+def special_key(cam: np.ndarray, key: str) -> bool:
+    """SpecialFunc (display_func.c:384-433): key in GLUT_SPECIAL."""
+    assert cam.dtype == CAMERA_DTYPE and cam.flags.c_contiguous
+    return bool(lib.oracle_special_key(_p(cam), GLUT_SPECIAL[key]))
 
 
 def path_passes(spheres, rnd, cam, width, height, lp, sid, vlp, colors=None, counter=None,

@@ -460,16 +460,98 @@ void oracle_path_passes(const Sphere *sp, unsigned n, const float *rnd, const Ca
     }
 }
 
+/* vnorm (vec.h:22) as it compiles in the reference's host C files (display_func.c is C, so
+ * `sqrt` is the double libm sqrt): l = (float)(1.f / sqrt((double)vdot)), one rounding. */
+static inline Vec vnorm_host(Vec v) { float l = (float)(1.f / sqrt((double)vdot(v, v))); return vsmul(l, v); }
+
 /* UpdateCamera display_func.c:177-190. */
 void oracle_update_camera(Camera *c, int width, int height)
 {
-    c->dir = vnorm(vsub(c->target, c->orig));
+    c->dir = vnorm_host(vsub(c->target, c->orig));
     const Vec up = vinit(0.f, 1.f, 0.f);
     const float fov = (float)((M_PI / 180.f) * 45.f);
-    c->x = vnorm(vxcross(c->dir, up));
+    c->x = vnorm_host(vxcross(c->dir, up));
     c->x = vsmul(width * fov / height, c->x);
-    c->y = vnorm(vxcross(c->x, c->dir));
+    c->y = vnorm_host(vxcross(c->x, c->dir));
     c->y = vsmul(fov, c->y);
+}
+
+/* KeyFunc camera keys display_func.c:276-336 (MOVE_STEP 10.0f).  Returns 1 when the reference
+ * calls ReInit(1) for the key (' ' too), 0 otherwise.  The camera is not re-derived here:
+ * ReInit -> UpdateCamera does that. */
+int oracle_key_camera(Camera *c, int key)
+{
+    const float step = 10.0f;
+    Vec d;
+    switch (key) {
+    case ' ':
+        return 1;
+    case 'a':                                            /* :291-298 */
+        d = vnorm_host(c->x);
+        d = vsmul(-step, d);
+        break;
+    case 'd':                                            /* :300-307 */
+        d = vnorm_host(c->x);
+        d = vsmul(step, d);
+        break;
+    case 'w':                                            /* :309-315 */
+        d = vsmul(step, c->dir);
+        break;
+    case 's':                                            /* :317-323 */
+        d = vsmul(-step, c->dir);
+        break;
+    case 'r':                                            /* :325-329 */
+        c->orig.y += step;
+        c->target.y += step;
+        return 1;
+    case 'f':                                            /* :330-334 */
+        c->orig.y -= step;
+        c->target.y -= step;
+        return 1;
+    default:
+        return 0;
+    }
+    c->orig = vadd(c->orig, d);
+    c->target = vadd(c->target, d);
+    return 1;
+}
+
+/* SpecialFunc display_func.c:384-433 with GLUT codes (LEFT 100, UP 101, RIGHT 102, DOWN 103,
+ * PAGE_UP 104, PAGE_DOWN 105).  ROTATE_STEP = 2.f*M_PI/180.f is a double expression, so the
+ * products and sums are double and each assignment rounds to float; the second line reads the
+ * component the first one already overwrote (Appendix A.9). */
+int oracle_special_key(Camera *c, int key)
+{
+    const double rs = 2.f * M_PI / 180.f;
+    Vec t;
+    switch (key) {
+    case 101:
+    case 103: {                                          /* UP :386-394, DOWN :396-404 */
+        const double a = key == 101 ? -rs : rs;
+        t = vsub(c->target, c->orig);
+        t.y = t.y * cos(a) + t.z * sin(a);
+        t.z = -t.y * sin(a) + t.z * cos(a);
+        c->target = vadd(t, c->orig);
+        return 1;
+    }
+    case 100:
+    case 102: {                                          /* LEFT :406-414, RIGHT :416-424 */
+        const double a = key == 100 ? -rs : rs;
+        t = vsub(c->target, c->orig);
+        t.x = t.x * cos(a) - t.z * sin(a);
+        t.z = t.x * sin(a) + t.z * cos(a);
+        c->target = vadd(t, c->orig);
+        return 1;
+    }
+    case 104:                                            /* :426-429 */
+        c->target.y += 10.0f;
+        return 1;
+    case 105:                                            /* :430-433 */
+        c->target.y -= 10.0f;
+        return 1;
+    default:
+        return 0;
+    }
 }
 
 /* toInt(vec.h:34) of one value -- lets tests check the product's threshold table. */

@@ -1,0 +1,117 @@
+"""ORACLE -- test infrastructure only.  Restatement of the reference's host control flow:
+the GLUT idle loop and key handlers driving the render path, on top of the CPU restatement.
+
+    IdleFunc        display_func.c:192-217  (flag == 1 -> light pass; flag > 1 -> path pass)
+    UpdateRendering smallpt_cpu.c:265-297   (sid = rand() % RAND_N; flag / vlp_index machine)
+    UpdateRendering2 smallpt_cpu.c:300-362  (MT table seeded current_sample*5 + light pass; flag=2)
+    ReInitScene     smallpt_cpu.c:365-371   (current_sample=0, flag=1, realloc, light pass)
+    ReInit          smallpt_cpu.c:373-387   (realloc, reinit_counter++, UpdateCamera,
+                                             light pass on even counts, one path pass)
+    KeyFunc         display_func.c:276-382, SpecialFunc display_func.c:384-437
+
+Buffers follow the documented fixes: AllocateBuffers zeroes the counter
+(smallpt_cpu.c:204) and the colors follow from `counter == 0` assigning; the MT table and
+dev_lp persist across a re-allocation (Appendix A.6) instead of being left uninitialised.
+`rand()` is glibc's, seeded 1 as by default (ctypes on libc.so.6).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import (CAMERA_DTYPE, RAND_N, SPHERE_DTYPE, key_camera, light_pass, mt607, path_passes,
+               special_key, update_camera)
+
+MAX_ITER = 3          # smallpt_cpu.c: flag cycles 2 -> 3 -> (vlp_index += MAX_VLP; 1 -> 2)
+MAX_VLP = 1
+
+
+class Session:
+    """One reference process: globals of smallpt_cpu.c / display_func.c as attributes."""
+
+    def __init__(self, spheres: np.ndarray, orig, target, width: int, height: int,
+                 rows: tuple[int, int] | None = None):
+        self._libc = ctypes.CDLL("libc.so.6")
+        self._libc.srand(1)
+        self.spheres = np.ascontiguousarray(spheres.astype(SPHERE_DTYPE, copy=True))
+        self.width, self.height = width, height          # internal (+1 applied by caller)
+        self.camera = update_camera(orig, target, width, height)
+        self.rows = rows
+        self.current_sample = 0
+        self.reinit_counter = 0
+        self.current_sphere = 0
+        self.flag = 1
+        self.vlp_index = MAX_VLP
+        self.rnd = None
+        self.lp = None
+        self.colors = np.zeros((height, width, 3), np.float32)
+        self.counter = np.zeros((height, width), np.uint32)
+        self.pixels = np.zeros((height, width, 4), np.uint8)
+
+    # AllocateBuffers smallpt_cpu.c:153-237 (the spheres are re-uploaded; counter := 0)
+    def AllocateBuffers(self):
+        self.counter[...] = 0
+
+    def UpdateRendering2(self):
+        self.rnd = mt607(self.current_sample * 5)
+        self.lp = light_pass(self.spheres, self.rnd, self.current_sample)
+        self.flag = 2
+
+    def UpdateRendering(self):
+        sid = self._libc.rand() % RAND_N
+        vlp = self.vlp_index % 4096                      # Appendix A.3 wrap
+        self.colors, self.counter, self.pixels = path_passes(
+            self.spheres, self.rnd, self.camera, self.width, self.height, self.lp,
+            np.array([sid], np.uint32), np.array([vlp], np.int32),
+            self.colors, self.counter, self.pixels, rows=self.rows)
+        self.current_sample += 1
+        if self.flag == MAX_ITER:
+            self.vlp_index += MAX_VLP
+            self.flag = 1
+        if self.flag < MAX_ITER:
+            self.flag += 1
+
+    def IdleFunc(self):
+        if self.flag == 1:
+            self.UpdateRendering2()
+        if self.flag > 1:
+            self.UpdateRendering()
+
+    def ReInitScene(self):
+        self.current_sample = 0
+        self.flag = 1
+        self.AllocateBuffers()
+        self.UpdateRendering2()
+
+    def ReInit(self, realloc: int = 1):
+        if realloc:
+            self.AllocateBuffers()
+        self.reinit_counter += 1
+        c = update_camera(self.camera["orig"][0], self.camera["target"][0], self.width, self.height)
+        self.camera = c
+        self.current_sample = 0
+        if self.reinit_counter % 2 == 0:
+            self.UpdateRendering2()
+        self.UpdateRendering()
+
+    def KeyFunc(self, key: str):
+        n = len(self.spheres)
+        if key == "+":
+            self.current_sphere = (self.current_sphere + 1) % n
+            self.ReInitScene()
+        elif key == "-":
+            self.current_sphere = (self.current_sphere + (n - 1)) % n
+            self.ReInitScene()
+        elif key in "468293" and len(key) == 1:          # display_func.c:347-370
+            p = self.spheres[self.current_sphere]["p"]
+            axis, sign = {"4": (0, -1), "6": (0, 1), "8": (2, -1), "2": (2, 1),
+                          "9": (1, 1), "3": (1, -1)}[key]
+            p[axis] = np.float32(p[axis] + np.float32(sign) * (np.float32(0.5) * np.float32(10.0)))
+            self.ReInitScene()
+        elif key_camera(self.camera, key):
+            self.ReInit(1)
+
+    def SpecialFunc(self, key: str):
+        if special_key(self.camera, key):
+            self.ReInit(1)
