@@ -29,6 +29,11 @@ WORK = {
     "caustic": {"sphere_tests": 5.1332, "segments": 1.5151, "diffuse": 0.4516, "refr": 0.0638, "rng_reads": 3.8704},
     "simple": {"sphere_tests": 8.7195, "segments": 1.5033, "diffuse": 0.5039, "refr": 0.0, "rng_reads": 4.0156},
     "synthetic64": {"sphere_tests": 609.1571, "segments": 6.9145, "diffuse": 5.6567, "refr": 0.908, "rng_reads": 25.5348},
+    # large scenes: counted on every 36th row (the full frame takes the oracle a minute)
+    "complex": {"sphere_tests": 1527.9675, "segments": 1.6307, "diffuse": 0.6397, "refr": 0.0, "rng_reads": 4.5589,
+                "_rows_step": 36},
+    "mod_cornell": {"sphere_tests": 11602.571, "segments": 6.8993, "diffuse": 6.7583, "refr": 0.1145,
+                    "rng_reads": 29.1478, "_rows_step": 36},
 }
 # FLOP model per primitive (DESIGN.md "Roofline"): sphere test 18, segment shading 28,
 # diffuse vertex (NEE to one light + VLP + new direction) 153, refraction 40, camera ray +
@@ -85,6 +90,9 @@ def main():
     ap.add_argument("--height", type=int, default=1080, help="CLI height (internal = +1)")
     ap.add_argument("--passes", type=int, default=16, help="passes per step per GPU share")
     ap.add_argument("--band-rows", type=int, default=8)
+    ap.add_argument("--traversal", default="auto", choices=["auto", "brute", "bvh"],
+                    help="sphere traversal for >16-sphere scenes (results identical)")
+    ap.add_argument("--streams", type=int, default=0, help="pass streams per pixel (0 = auto)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -109,6 +117,8 @@ def main():
     g.update_camera(cam, W, H)
     r = g.Renderer(sp, W, H, cam, device=local)
     r.set_shard(rank, world, args.band_rows)
+    r.set_traversal(args.traversal)
+    r.set_streams(args.streams)
     r.light_pass(0)                                           # UpdateRendering2
     sched = g.PassScheduler()
     sched.light()
@@ -200,7 +210,7 @@ def main():
                        "scene": args.scene, "width": W, "height": H, "passes_per_step": per_step,
                        "spp_total": per_step * (args.warmup + args.steps),
                        "parallelism": f"pixel bands x{world} ({args.band_rows}-row, interleaved)",
-                       "pass_streams": r.last_streams},
+                       "pass_streams": r.last_streams, "traversal": r.last_traversal},
             "device_ms_per_step": round(dev_ms / args.steps, 3),
             "roofline": roofline, "valu": valu, "cpu_baseline": cpu,
         }

@@ -22,7 +22,7 @@ from ._lib import (BDPT_OK, COUNTER_CAP, DEFAULT_DAT, DIFF, KEY_DOWN, KEY_LEFT, 
 
 __all__ = [
     "Vec", "Sphere", "Camera", "LightPath", "Renderer", "SmallPT", "PassScheduler", "read_scene",
-    "default_scene", "update_camera", "camera_key", "sphere_key", "save_ppm", "glibc_rand",
+    "default_scene", "update_camera", "camera_key", "sphere_key", "save_ppm", "ppm_name", "glibc_rand",
     "spheres_to_array", "RAND_N", "LIGHT_POINTS", "COUNTER_CAP", "DIFF", "SPEC", "REFR", "LITE",
     "SCENE_DIR", "DEFAULT_DAT", "BdptError",
 ]
@@ -102,13 +102,21 @@ def sphere_key(spheres: np.ndarray, current: int, key: str) -> bool:
     return bool(lib.bdpt_sphere_key(_sphere_ptr(spheres), len(spheres), int(current), ord(key)))
 
 
-def save_ppm(path: str, rgba: np.ndarray) -> None:
-    """SavePPM (smallpt_cpu.c:239-262): ASCII P3, rows bottom-up."""
+def save_ppm(path: str, rgba: np.ndarray, binary: bool = False) -> None:
+    """SavePPM (smallpt_cpu.c:239-262): ASCII P3, rows bottom-up; binary=True writes P6."""
     rgba = np.ascontiguousarray(rgba, dtype=np.uint8)
     h, w = rgba.shape[:2]
-    rc = lib.bdpt_save_ppm(os.fsencode(path), _ptr(rgba), w, h)
+    fn = lib.bdpt_save_ppm_binary if binary else lib.bdpt_save_ppm
+    rc = fn(os.fsencode(path), _ptr(rgba), w, h)
     if rc != BDPT_OK:
         raise BdptError(rc, f"cannot write {path}")
+
+
+def ppm_name(total_time: float, current_sample: int) -> str:
+    """SavePPM's file name (smallpt_cpu.c:245): max1_secondi<total_time %.3f>_exe<sample>.ppm."""
+    buf = ctypes.create_string_buffer(128)
+    lib.bdpt_ppm_name(buf, len(buf), float(total_time), int(current_sample))
+    return buf.value.decode()
 
 
 def glibc_rand(n: int, seed: int = 1) -> np.ndarray:
@@ -206,6 +214,18 @@ class Renderer:
     @property
     def last_streams(self) -> int:
         return int(lib.bdpt_last_streams(self._h))
+
+    def set_traversal(self, mode: str) -> None:
+        """'auto' (BVH when the scene has one), 'brute' (every sphere) or 'bvh'."""
+        self._chk(lib.bdpt_set_traversal(self._h, {"auto": 0, "brute": 1, "bvh": 2}[mode]))
+
+    @property
+    def has_bvh(self) -> bool:
+        return bool(lib.bdpt_scene_has_bvh(self._h))
+
+    @property
+    def last_traversal(self) -> str:
+        return {1: "brute", 2: "bvh"}[int(lib.bdpt_last_traversal(self._h))]
 
     # -- work
     def generate_rand(self, seed: int) -> None:
@@ -325,7 +345,8 @@ class SmallPT:
         self.renderer.path_passes(sid, vlp)
         dt = time.perf_counter() - t0
         self.current_sample += npass
-        self.total_time += dt
+        # static float total_time; total_time += (float)elapsed (smallpt_cpu.c:35,283)
+        self.total_time = float(np.float32(np.float32(self.total_time) + np.float32(dt)))
         return self.width * self.height * npass / dt if dt > 0 else float("inf")
 
     def IdleFunc(self, npass: int = 1) -> None:              # display_func.c:192-217
@@ -372,8 +393,8 @@ class SmallPT:
     def pixels(self) -> np.ndarray:
         return self.renderer.read_pixels()
 
-    def SavePPM(self, path: Optional[str] = None) -> str:   # smallpt_cpu.c:239-262
+    def SavePPM(self, path: Optional[str] = None, binary: bool = False) -> str:   # smallpt_cpu.c:239-262
         if path is None:
-            path = "max%d_secondi%.3f_exe%d.ppm" % (1, self.total_time, self.current_sample)
-        save_ppm(path, self.pixels())
+            path = ppm_name(self.total_time, self.current_sample)
+        save_ppm(path, self.pixels(), binary)
         return path

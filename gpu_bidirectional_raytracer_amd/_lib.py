@@ -69,6 +69,9 @@ _SIGS = [
     ("bdpt_set_shard", ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     ("bdpt_set_streams", ctypes.c_int, [_P, ctypes.c_int]),
     ("bdpt_last_streams", ctypes.c_int, [_P]),
+    ("bdpt_set_traversal", ctypes.c_int, [_P, ctypes.c_int]),
+    ("bdpt_scene_has_bvh", ctypes.c_int, [_P]),
+    ("bdpt_last_traversal", ctypes.c_int, [_P]),
     ("bdpt_light_pass", ctypes.c_int, [_P, ctypes.c_int]),
     ("bdpt_generate_rand", ctypes.c_int, [_P, ctypes.c_uint]),
     ("bdpt_path_passes", ctypes.c_int, [_P, _P, _P, ctypes.c_int]),
@@ -90,6 +93,8 @@ _SIGS = [
     ("bdpt_camera_key", ctypes.c_int, [ctypes.POINTER(Camera), ctypes.c_int]),
     ("bdpt_sphere_key", ctypes.c_int, [ctypes.POINTER(Sphere), ctypes.c_uint, ctypes.c_int, ctypes.c_int]),
     ("bdpt_save_ppm", ctypes.c_int, [ctypes.c_char_p, _P, ctypes.c_int, ctypes.c_int]),
+    ("bdpt_save_ppm_binary", ctypes.c_int, [ctypes.c_char_p, _P, ctypes.c_int, ctypes.c_int]),
+    ("bdpt_ppm_name", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.c_float, ctypes.c_int]),
     ("bdpt_gamma_thresholds", None, [_P]),
     ("bdpt_srand", None, [ctypes.POINTER(RandState), ctypes.c_uint]),
     ("bdpt_rand", ctypes.c_int, [ctypes.POINTER(RandState)]),

@@ -16,6 +16,7 @@
 #define BDPT_DEV_N_PER_RNG 1876
 #define BDPT_DEV_LIGHT_POINTS 4096
 #define BDPT_DEV_COUNTER_CAP 30000u
+#define BDPT_DEV_BVH_EMISSIVE (1 << 30)   // BVH sphere id flag (bdpt_bvh.h kBvhEmissive)
 #define BDPT_DEV_DIFF 0
 #define BDPT_DEV_SPEC 1
 #define BDPT_DEV_REFR 2
@@ -70,6 +71,16 @@ struct bdpt_path_args {
     int streams;                    // pass streams S: lane (pixel, s) renders passes s, s+S, ...
     bdpt_dev_vec* rbuf;             // S > 1: per (pass, launched pixel) radiance, [npass][nloc]
     int nloc;                       // launched pixels per pass = gridDim.y * BDPT_BTH * W
+    // BVH traversal (large scenes, kernel table index 17; see bdpt_bvh.cpp)
+    const float4* bvh_nodes;        // 2 per node: {lo, skip}, {hi, leaf first|count<<24 or -1}
+    const float4* bvh_geom;         // BVH spheres in leaf order {p, rad^2}
+    const int* bvh_ids;             // sphere index | 1<<30 if emissive
+    const float4* big_geom;         // brute-force spheres (walls) {p, rad^2}
+    const int* big_ids;
+    const float4* mat;              // per sphere: {c, refl | emissive<<8}, {e, rad}, {p, 0}
+    int bvh_nn, bvh_ns, big_n;
+    float bvh_c[3], bvh_r;          // ball around every BVH sphere (per-ray margin)
+    float bvh_q;                    // 32u / smallest BVH radius (per-ray margin)
 };
 
 // Tile row of a workgroup row: identity, or the sub-th tile row of this shard's k-th band.

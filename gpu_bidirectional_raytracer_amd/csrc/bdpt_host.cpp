@@ -15,6 +15,9 @@
 
 #include "../../include/bdpt.h"
 #include "bdpt_device.h"
+#include "bdpt_bvh.h"
+
+static_assert(kBvhEmissive == BDPT_DEV_BVH_EMISSIVE, "BVH id flag");
 
 static_assert(sizeof(bdpt_vec) == 12, "Vec is 12 B (vec.h:4-6)");
 static_assert(sizeof(bdpt_ray) == 24, "Ray is 24 B (geom.h:9-11)");
@@ -27,7 +30,7 @@ static_assert(sizeof(bdpt_dev_vec) == sizeof(bdpt_vec), "colour layout");
 extern "C" __global__ void bdpt_mt607_kernel(const uint4*, unsigned, float*);
 extern "C" __global__ void bdpt_light_kernel(const bdpt_dev_sphere*, unsigned, const float*, int,
                                              bdpt_dev_lightpath*);
-extern "C" const void* bdpt_path_kernel_table[34];   // [(S > 1) * 17 + (n <= 16 ? n : 0)]
+extern "C" const void* bdpt_path_kernel_table[36];   // [(S > 1) * 18 + (BVH ? 17 : n <= 16 ? n : 0)]
 extern "C" __global__ void bdpt_pixels_kernel(const bdpt_dev_vec*, uchar4*, const float*, int);
 extern "C" __global__ void bdpt_accum_kernel(bdpt_path_args);
 
@@ -52,8 +55,15 @@ struct bdpt_ctx {
     int shard = 0, nshards = 1, band_rows = 8;
     int streams_req = 0;                // bdpt_set_streams: 0 = auto
     int last_streams = 1;               // S of the last path-pass launch
+    bool last_bvh = false;              // the last path-pass launch traversed the BVH
     int cus = 256;                      // compute units (auto stream count)
     bdpt_dev_vec* d_rbuf = nullptr;     // pass-stream radiance, [npass][nloc]
+    int traversal = BDPT_TRAVERSE_AUTO; // bdpt_set_traversal
+    bool has_bvh = false;               // the scene has a BVH (bdpt_bvh.cpp)
+    int bvh_nn = 0, bvh_ns = 0, big_n = 0;
+    float bvh_c[3] = {0.f, 0.f, 0.f}, bvh_r = 0.f, bvh_q = 0.f;
+    float4 *d_bvh_nodes = nullptr, *d_bvh_geom = nullptr, *d_big_geom = nullptr, *d_mat = nullptr;
+    int *d_bvh_ids = nullptr, *d_big_ids = nullptr;
     size_t rbuf_cap = 0;                // elements
     uint4* d_params = nullptr;          // 4096 x {matrix_a, mask_b, mask_c, seed}
     float* d_rand = nullptr;
@@ -137,12 +147,55 @@ static int upload_scene(bdpt_ctx* c) {
         HIPCHK(c, hipMemcpyAsync(c->d_lights, c->lights.data(), sizeof(int) * c->lights.size(),
                                  hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+
+    // large scenes: BVH over the ordinary spheres + per-sphere material table in HBM
+    void* old[] = {c->d_bvh_nodes, c->d_bvh_geom, c->d_big_geom, c->d_mat, c->d_bvh_ids, c->d_big_ids};
+    for (void* b : old)
+        if (b) HIPCHK(c, hipFree(b));
+    c->d_bvh_nodes = c->d_bvh_geom = c->d_big_geom = c->d_mat = nullptr;
+    c->d_bvh_ids = c->d_big_ids = nullptr;
+    c->has_bvh = false;
+    bdpt_bvh bvh;
+    if (n > 16 && bdpt_build_bvh(c->spheres.data(), n, &bvh)) {
+        std::vector<float4> mat(3 * (size_t)n);
+        for (unsigned i = 0; i < n; i++) {
+            const bdpt_dev_sphere& d = ds[i];
+            const bool emis = !(d.ex == 0.f && d.ey == 0.f && d.ez == 0.f);
+            mat[3 * i] = make_float4(d.cx, d.cy, d.cz, bdpt_bits_as_float(d.refl | (emis ? 256 : 0)));
+            mat[3 * i + 1] = make_float4(d.ex, d.ey, d.ez, d.rad);
+            mat[3 * i + 2] = make_float4(d.px, d.py, d.pz, 0.f);
+        }
+        c->bvh_nn = (int)bvh.nodes.size() / 2;
+        c->bvh_ns = (int)bvh.geom.size();
+        c->big_n = (int)bvh.big_geom.size();
+        for (int k = 0; k < 3; k++) c->bvh_c[k] = bvh.c_root[k];
+        c->bvh_r = bvh.r_root;
+        c->bvh_q = bvh.q;
+        HIPCHK(c, hipMalloc(&c->d_bvh_nodes, sizeof(float4) * bvh.nodes.size()));
+        HIPCHK(c, hipMalloc(&c->d_bvh_geom, sizeof(float4) * bvh.geom.size()));
+        HIPCHK(c, hipMalloc(&c->d_bvh_ids, sizeof(int) * bvh.ids.size()));
+        HIPCHK(c, hipMalloc(&c->d_mat, sizeof(float4) * mat.size()));
+        HIPCHK(c, hipMemcpy(c->d_bvh_nodes, bvh.nodes.data(), sizeof(float4) * bvh.nodes.size(), hipMemcpyHostToDevice));
+        HIPCHK(c, hipMemcpy(c->d_bvh_geom, bvh.geom.data(), sizeof(float4) * bvh.geom.size(), hipMemcpyHostToDevice));
+        HIPCHK(c, hipMemcpy(c->d_bvh_ids, bvh.ids.data(), sizeof(int) * bvh.ids.size(), hipMemcpyHostToDevice));
+        HIPCHK(c, hipMemcpy(c->d_mat, mat.data(), sizeof(float4) * mat.size(), hipMemcpyHostToDevice));
+        if (c->big_n) {
+            HIPCHK(c, hipMalloc(&c->d_big_geom, sizeof(float4) * bvh.big_geom.size()));
+            HIPCHK(c, hipMalloc(&c->d_big_ids, sizeof(int) * bvh.big_ids.size()));
+            HIPCHK(c, hipMemcpy(c->d_big_geom, bvh.big_geom.data(), sizeof(float4) * bvh.big_geom.size(),
+                                hipMemcpyHostToDevice));
+            HIPCHK(c, hipMemcpy(c->d_big_ids, bvh.big_ids.data(), sizeof(int) * bvh.big_ids.size(),
+                                hipMemcpyHostToDevice));
+        }
+        c->has_bvh = true;
+    }
     return BDPT_OK;
 }
 
 static void release(bdpt_ctx* c) {
     void* bufs[] = {c->d_params, c->d_rand, c->d_lp, c->d_sph, c->d_lights, c->d_geom, c->d_lightrec, c->d_colors,
-                    c->d_counter, c->d_pixels, c->d_thr, c->d_sid, c->d_vlp, c->d_rbuf};
+                    c->d_counter, c->d_pixels, c->d_thr, c->d_sid, c->d_vlp, c->d_rbuf, c->d_bvh_nodes,
+                    c->d_bvh_geom, c->d_big_geom, c->d_mat, c->d_bvh_ids, c->d_big_ids};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -276,6 +329,20 @@ int bdpt_set_streams(bdpt_ctx* c, int streams) {
 
 int bdpt_last_streams(const bdpt_ctx* c) { return c ? c->last_streams : BDPT_EINVAL; }
 
+int bdpt_set_traversal(bdpt_ctx* c, int mode) {
+    if (!c) return BDPT_EINVAL;
+    if (mode != BDPT_TRAVERSE_AUTO && mode != BDPT_TRAVERSE_BRUTE && mode != BDPT_TRAVERSE_BVH)
+        return fail(c, BDPT_EINVAL, "bdpt_set_traversal: bad mode %d", mode);
+    c->traversal = mode;
+    return BDPT_OK;
+}
+
+int bdpt_scene_has_bvh(const bdpt_ctx* c) { return c ? (int)c->has_bvh : BDPT_EINVAL; }
+
+int bdpt_last_traversal(const bdpt_ctx* c) {
+    return c ? (c->last_bvh ? BDPT_TRAVERSE_BVH : BDPT_TRAVERSE_BRUTE) : BDPT_EINVAL;
+}
+
 int bdpt_generate_rand(bdpt_ctx* c, unsigned seed) {
     if (!c) return BDPT_EINVAL;
     HIPCHK(c, hipSetDevice(c->device));
@@ -401,7 +468,17 @@ int bdpt_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int npass
     if (S < 1) S = 1;
     a.streams = S;
     c->last_streams = S;
-    const void* kern = bdpt_path_kernel_table[(S > 1) * 17 + (a.n <= 16 ? a.n : 0)];
+    const bool bvh = c->has_bvh && c->traversal != BDPT_TRAVERSE_BRUTE;
+    const void* kern = bdpt_path_kernel_table[(S > 1) * 18 + (bvh ? 17 : (a.n <= 16 ? a.n : 0))];
+    if (bvh) {
+        a.bvh_nodes = c->d_bvh_nodes; a.bvh_geom = c->d_bvh_geom; a.bvh_ids = c->d_bvh_ids;
+        a.big_geom = c->d_big_geom; a.big_ids = c->d_big_ids; a.mat = c->d_mat;
+        a.bvh_nn = c->bvh_nn; a.bvh_ns = c->bvh_ns; a.big_n = c->big_n;
+        for (int k = 0; k < 3; k++) a.bvh_c[k] = c->bvh_c[k];
+        a.bvh_r = c->bvh_r;
+        a.bvh_q = c->bvh_q;
+    }
+    c->last_bvh = bvh;
     if (S > 1) {
         const int cmax = npass < chunk ? npass : chunk;
         const size_t need = (size_t)cmax * (size_t)lanes;
@@ -421,9 +498,12 @@ int bdpt_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int npass
         a.sid = c->d_sid + p0;
         a.vlp = c->d_vlp + p0;
         a.npass = npass - p0 < chunk ? npass - p0 : chunk;
-        // spheres (4 tables) + per-pass VLPs + camera + 4 wave shadow queues + results + sids
-        const size_t smem = sizeof(float4) * (4 * (size_t)a.n + 3 * (size_t)a.npass + 5 + 4 * 128 * 2)
-                            + sizeof(unsigned) * (4 * 128 + (size_t)a.npass);
+        // scene tables (4 per sphere, or the BVH: 2 per node + 1 per sphere) + per-pass VLPs +
+        // camera + 4 wave shadow queues + results + sids (+ BVH sphere ids)
+        const size_t tab = bvh ? 2 * (size_t)a.bvh_nn + a.bvh_ns + a.big_n : 4 * (size_t)a.n;
+        const size_t ids = bvh ? (size_t)a.bvh_ns + a.big_n : 0;
+        const size_t smem = sizeof(float4) * (tab + 3 * (size_t)a.npass + 5 + 4 * 128 * 2)
+                            + sizeof(unsigned) * (4 * 128 + (size_t)a.npass + ids);
         if (smem > 160 * 1024)
             return fail(c, BDPT_EINVAL, "bdpt_path_passes: scene too large for LDS (%u spheres)", a.n);
         void* kargs[] = {&a};

@@ -255,32 +255,94 @@ __device__ __forceinline__ void wave_lds_fence() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
 }
+
+// ---- BVH traversal (large scenes; tree built by bdpt_bvh.cpp) --------------------------------
+// The float sphere test (SphereIntersectDevice) differs from the exact root of its own formula
+// by at most ~sqrt(20u)*(|op|+r) ~ 1.1e-3*(|op|+r) (u = 2^-24; the det cancellation under the
+// sqrt dominates), and a float hit on an exactly-missed sphere lies within the same distance of
+// it.  The float direction is unit only to ~8u, which acts like a radius error of ~8u*D^2/r.
+// Every box is therefore widened by m = D*(kBvhK + q*D), D = |o - c_root| + r_root >= |op|+r
+// for all BVH spheres, q = 32u / (smallest BVH radius) -- 3.6x and 4x those bounds;
+// tests/test_bvh_margin.py checks on worst-case rays that every float hit point lies within
+// m/2 of its sphere's box -- and a box is skipped only if entered beyond tmax + m or left
+// before -m.
+constexpr float kBvhK = 4e-3f;
+constexpr int kBvhEmissive = BDPT_DEV_BVH_EMISSIVE;
+constexpr int kBvhIdMask = BDPT_DEV_BVH_EMISSIVE - 1;
+
+struct bvh_ray {
+    f3 olo, ohi, inv;
+    float m;
+};
+
+__device__ __forceinline__ bvh_ray bvh_setup(const bdpt_path_args& a, f3 o, f3 d) {
+    const f3 dc = sub(o, mk(a.bvh_c[0], a.bvh_c[1], a.bvh_c[2]));
+    const float D = __builtin_amdgcn_sqrtf(dot(dc, dc) * 1.00001f) * 1.00001f + a.bvh_r;
+    bvh_ray r;
+    r.m = D * (kBvhK + a.bvh_q * D);
+    r.olo = mk(o.x + r.m, o.y + r.m, o.z + r.m);    // lo - (o + m) = (lo - m) - o
+    r.ohi = mk(o.x - r.m, o.y - r.m, o.z - r.m);    // hi - (o - m) = (hi + m) - o
+    const float e = 1e-20f;
+    r.inv = mk(1.f / (fabsf(d.x) > e ? d.x : copysignf(e, d.x)),
+               1.f / (fabsf(d.y) > e ? d.y : copysignf(e, d.y)),
+               1.f / (fabsf(d.z) > e ? d.z : copysignf(e, d.z)));
+    return r;
+}
+
+__device__ __forceinline__ bool bvh_box(float4 lo, float4 hi, const bvh_ray& r, float tmax) {
+    const float x0 = (lo.x - r.olo.x) * r.inv.x, x1 = (hi.x - r.ohi.x) * r.inv.x;
+    const float y0 = (lo.y - r.olo.y) * r.inv.y, y1 = (hi.y - r.ohi.y) * r.inv.y;
+    const float z0 = (lo.z - r.olo.z) * r.inv.z, z1 = (hi.z - r.ohi.z) * r.inv.z;
+    const float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
+    const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
+    return tn <= tf && tf >= -r.m && tn <= tmax + r.m;
+}
 }  // namespace
 
 #ifndef BDPT_WAVES_PER_SIMD
 #define BDPT_WAVES_PER_SIMD 5
 #endif
+// BVH scenes hold ~30 KB of tree in LDS per workgroup (4 per CU): 4 waves/SIMD, 128 VGPRs.
 template <int N, bool STREAMS>
-__global__ __launch_bounds__(256, BDPT_WAVES_PER_SIMD) void bdpt_path_kernel_t(bdpt_path_args a) {
+__global__ __launch_bounds__(256, N < 0 ? 4 : BDPT_WAVES_PER_SIMD) void bdpt_path_kernel_t(bdpt_path_args a) {
     extern __shared__ float4 smem[];
+    constexpr bool kBVH = N < 0;      // large scene: walls brute force + BVH (bdpt_bvh.cpp)
     const int n = N > 0 ? N : (int)a.n;
     constexpr int kUnroll = N > 0 ? N : 1;
+    const int ntab = kBVH ? 2 * a.bvh_nn + a.bvh_ns + a.big_n : 4 * n;
     float4* C = smem;                 // {cx, cy, cz, bits(refl | emissive<<8)}
     float4* E = smem + n;             // {ex, ey, ez, rad}
     float4* P = smem + 2 * n;         // {px, py, pz, 0}  (hit normal)
     float4* G = smem + 3 * n;         // {px, py, pz, rad^2}  (N == 0 traversal)
-    float4* V = smem + 4 * n;         // per pass: VLP {hx,hy,hz,rx}{ry,rz,nx,ny}{nz,-,-,-}
+    float4* ND = smem;                // BVH: nodes (2 float4 each)
+    float4* SG = ND + 2 * a.bvh_nn;   // BVH: sphere geometry in leaf order
+    float4* BG = SG + a.bvh_ns;       // BVH: brute-force (wall) geometry
+    float4* V = smem + ntab;          // per pass: VLP {hx,hy,hz,rx}{ry,rz,nx,ny}{nz,-,-,-}
     float4* K = V + 3 * a.npass;      // camera constants (5 float4)
     float4* Q = K + 5;                // shadow queues: 4 waves x kQueue x 2 float4
     unsigned* R = (unsigned*)(Q + 4 * kQueue * 2);    // shadow results: 4 x kQueue
     unsigned* SID = R + 4 * kQueue;   // per pass sid
-    for (int s = threadIdx.x; s < n; s += 256) {
-        const bdpt_dev_sphere S = a.sph[s];
-        const bool emis = !(S.ex == 0.f && S.ey == 0.f && S.ez == 0.f);
-        C[s] = make_float4(S.cx, S.cy, S.cz, __int_as_float(S.refl | (emis ? 256 : 0)));
-        E[s] = make_float4(S.ex, S.ey, S.ez, S.rad);
-        P[s] = make_float4(S.px, S.py, S.pz, 0.f);
-        G[s] = make_float4(S.px, S.py, S.pz, S.rr);
+    int* SI = (int*)(SID + a.npass);  // BVH: sphere ids (| emissive flag), leaf order
+    int* BI = SI + a.bvh_ns;          // BVH: wall ids
+    if constexpr (kBVH) {
+        for (int q = threadIdx.x; q < 2 * a.bvh_nn; q += 256) ND[q] = a.bvh_nodes[q];
+        for (int q = threadIdx.x; q < a.bvh_ns; q += 256) {
+            SG[q] = a.bvh_geom[q];
+            SI[q] = a.bvh_ids[q];
+        }
+        for (int q = threadIdx.x; q < a.big_n; q += 256) {
+            BG[q] = a.big_geom[q];
+            BI[q] = a.big_ids[q];
+        }
+    } else {
+        for (int s = threadIdx.x; s < n; s += 256) {
+            const bdpt_dev_sphere S = a.sph[s];
+            const bool emis = !(S.ex == 0.f && S.ey == 0.f && S.ez == 0.f);
+            C[s] = make_float4(S.cx, S.cy, S.cz, __int_as_float(S.refl | (emis ? 256 : 0)));
+            E[s] = make_float4(S.ex, S.ey, S.ez, S.rad);
+            P[s] = make_float4(S.px, S.py, S.pz, 0.f);
+            G[s] = make_float4(S.px, S.py, S.pz, S.rr);
+        }
     }
     for (int q = threadIdx.x; q < a.npass; q += 256) {
         const bdpt_dev_lightpath L = a.lp[a.vlp[q] & (BDPT_DEV_LIGHT_POINTS - 1)];
@@ -305,6 +367,10 @@ __global__ __launch_bounds__(256, BDPT_WAVES_PER_SIMD) void bdpt_path_kernel_t(b
         if constexpr (N > 0) return (a.emis_mask >> s) & 1u;
         else return (__float_as_int(C[s].w) & 256) != 0;
     };
+    // per-lane hit data: LDS tables, or (BVH scenes, too large for LDS) the global copy
+    auto tabC = [&](int s) -> float4 { if constexpr (kBVH) return a.mat[3 * s]; else return C[s]; };
+    auto tabE = [&](int s) -> float4 { if constexpr (kBVH) return a.mat[3 * s + 1]; else return E[s]; };
+    auto tabP = [&](int s) -> float4 { if constexpr (kBVH) return a.mat[3 * s + 2]; else return P[s]; };
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int x = blockIdx.x * BDPT_BTW + (wave % BDPT_BLOCK_WX) * BDPT_WTW + (lane % BDPT_WTW);
@@ -370,23 +436,48 @@ __global__ __launch_bounds__(256, BDPT_WAVES_PER_SIMD) void bdpt_path_kernel_t(b
             // closest hit, scanning from the last sphere down (device.cu:106-124)
             float t = 1e20f;
             int id = -1;
+            if constexpr (kBVH) {
+                // walls by brute force, then the BVH; equal distances go to the higher index,
+                // which is what the reference's downward scan with `d < t` yields
+                for (int q = a.big_n - 1; q >= 0; --q) {
+                    const float d = sphere_isect_inf(BG[q], ro, rd);
+                    const int s = BI[q] & kBvhIdMask;
+                    if (d < t || (d == t && s > id)) { t = d; id = s; }
+                }
+                const bvh_ray br = bvh_setup(a, ro, rd);
+                int node = 0;
+                while (node < a.bvh_nn) {
+                    const float4 lo = ND[2 * node], hi = ND[2 * node + 1];
+                    const int info = __float_as_int(hi.w);
+                    if (!bvh_box(lo, hi, br, t)) { node = __float_as_int(lo.w); continue; }
+                    if (info < 0) { node++; continue; }
+                    const int first = info & 0xffffff, end = first + (info >> 24);
+                    for (int k = first; k < end; k++) {
+                        const float d = sphere_isect_inf(SG[k], ro, rd);
+                        const int s = SI[k] & kBvhIdMask;
+                        if (d < t || (d == t && s > id)) { t = d; id = s; }
+                    }
+                    node = __float_as_int(lo.w);
+                }
+            } else {
 #pragma unroll kUnroll
-            for (int s = n - 1; s >= 0; --s) {
-                const float d = sphere_isect_inf(geom(s), ro, rd);
-                if (d < t) { t = d; id = s; }
+                for (int s = n - 1; s >= 0; --s) {
+                    const float d = sphere_isect_inf(geom(s), ro, rd);
+                    if (d < t) { t = d; id = s; }
+                }
             }
             done = id < 0;
             if (!done) {
-                const float4 cm = C[id];
+                const float4 cm = tabC(id);
                 const int mat = __float_as_int(cm.w);
-                const float4 pc = P[id];
+                const float4 pc = tabP(id);
                 const f3 hit = add(ro, smul(t, rd));
                 const f3 normal = norm(sub(hit, mk(pc.x, pc.y, pc.z)));
                 const float dp = dot(normal, rd);
                 nl = dp > 0 ? mk(-normal.x, -normal.y, -normal.z) : normal;   // (-1*sign(dp))*n, exact
                 if (mat & 256) {                                         // emitter (:651-661)
                     if (specular) {
-                        const float4 em = E[id];
+                        const float4 em = tabE(id);
                         rad = add(rad, mul(thr, smul(fabsf(dp), mk(em.x, em.y, em.z))));
                     }
                     done = true;
@@ -508,11 +599,32 @@ __global__ __launch_bounds__(256, BDPT_WAVES_PER_SIMD) void bdpt_path_kernel_t(b
                         occ = r0.w < -1e30f || vac;
                         if (0)
 #endif
+                        if constexpr (kBVH) {                             // IntersectP(Vacuum)Device
+                            for (int q = 0; q < a.big_n && !occ; q++) {
+                                const float dd = sphere_isect_inf(BG[q], o, d);
+                                if (dd < r0.w && !(vac && (BI[q] & kBvhEmissive))) occ = 1;
+                            }
+                            const bvh_ray br = bvh_setup(a, o, d);
+                            int node = occ ? a.bvh_nn : 0;
+                            while (node < a.bvh_nn) {
+                                const float4 lo = ND[2 * node], hi = ND[2 * node + 1];
+                                const int info = __float_as_int(hi.w);
+                                if (!bvh_box(lo, hi, br, r0.w)) { node = __float_as_int(lo.w); continue; }
+                                if (info < 0) { node++; continue; }
+                                const int first = info & 0xffffff, end = first + (info >> 24);
+                                for (int k = first; k < end; k++) {
+                                    const float dd = sphere_isect_inf(SG[k], o, d);
+                                    if (dd < r0.w && !(vac && (SI[k] & kBvhEmissive))) { occ = 1; break; }
+                                }
+                                node = occ ? a.bvh_nn : __float_as_int(lo.w);
+                            }
+                        } else {
 #pragma unroll kUnroll
                         for (int s = n - 1; s >= 0; --s) {                // IntersectP(Vacuum)Device
                             const float dd = sphere_isect_inf(geom(s), o, d);
                             // early exit (measured +2% over a branch-free loop)
                             if (dd < r0.w && !(vac && emissive(s))) { occ = 1; break; }
+                        }
                         }
                         SR[idx] = occ;
                     }
@@ -573,12 +685,13 @@ __global__ __launch_bounds__(256, BDPT_WAVES_PER_SIMD) void bdpt_path_kernel_t(b
     a.pixels[i] = bdpt_dev_to_rgba(col.x, col.y, col.z, a.gamma_thr);
 }
 
-// host-side launch table: [streams * 17 + sphere count], count 0 = generic LDS traversal
+// host-side launch table: [streams * 18 + k], k = sphere count (0 = generic LDS traversal) or 17 = BVH
 #define BDPT_K(NN, ST) (const void*)&bdpt_path_kernel_t<NN, ST>
 #define BDPT_ROW(ST) BDPT_K(0, ST), BDPT_K(1, ST), BDPT_K(2, ST), BDPT_K(3, ST), BDPT_K(4, ST), \
     BDPT_K(5, ST), BDPT_K(6, ST), BDPT_K(7, ST), BDPT_K(8, ST), BDPT_K(9, ST), BDPT_K(10, ST), \
-    BDPT_K(11, ST), BDPT_K(12, ST), BDPT_K(13, ST), BDPT_K(14, ST), BDPT_K(15, ST), BDPT_K(16, ST)
-extern "C" const void* bdpt_path_kernel_table[34] = {BDPT_ROW(false), BDPT_ROW(true)};
+    BDPT_K(11, ST), BDPT_K(12, ST), BDPT_K(13, ST), BDPT_K(14, ST), BDPT_K(15, ST), BDPT_K(16, ST), \
+    BDPT_K(-1, ST)
+extern "C" const void* bdpt_path_kernel_table[36] = {BDPT_ROW(false), BDPT_ROW(true)};
 #undef BDPT_ROW
 #undef BDPT_K
 

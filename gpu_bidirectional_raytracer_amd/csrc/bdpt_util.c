@@ -194,6 +194,38 @@ int bdpt_save_ppm(const char *path, const unsigned char *rgba, int w, int h)
     return fclose(f) == 0 ? BDPT_OK : BDPT_EIO;
 }
 
+/* Binary variant (P6): same header numbers and bottom-up row order, raw RGB bytes. */
+int bdpt_save_ppm_binary(const char *path, const unsigned char *rgba, int w, int h)
+{
+    if (!path || !rgba || w <= 0 || h <= 0) return BDPT_EINVAL;
+    FILE *f = fopen(path, "wb");
+    if (!f) {
+        fprintf(stderr, "Failed to open image file: %s\n", path);
+        return BDPT_EIO;
+    }
+    fprintf(f, "P6\n%d %d\n%d\n", w, h, 255);
+    unsigned char *row = malloc(3 * (size_t)w);
+    int ok = row != NULL;
+    for (int y = h - 1; ok && y >= 0; --y) {
+        const unsigned char *p = rgba + 4 * (size_t)y * w;
+        for (int x = 0; x < w; ++x, p += 4) {
+            row[3 * x] = p[0]; row[3 * x + 1] = p[1]; row[3 * x + 2] = p[2];
+        }
+        ok = fwrite(row, 3, (size_t)w, f) == (size_t)w;
+    }
+    free(row);
+    return (fclose(f) == 0 && ok) ? BDPT_OK : BDPT_EIO;
+}
+
+/* SavePPM's file name smallpt_cpu.c:245 "max%d_secondi%.3f_exe%d.ppm" (MAX_VLP = 1), bounded
+ * (the reference's name[32] overflows once total_time >= 1000 s, Appendix A.10).  Returns the
+ * length snprintf reports. */
+int bdpt_ppm_name(char *buf, int size, float total_time, int current_sample)
+{
+    if (!buf || size <= 0) return BDPT_EINVAL;
+    return snprintf(buf, (size_t)size, "max%d_secondi%.3f_exe%d.ppm", 1, total_time, current_sample);
+}
+
 /* glibc random_r TYPE_3 (x**31 + x**3 + 1), the generator behind rand(). */
 void bdpt_srand(bdpt_rand_state *st, unsigned seed)
 {

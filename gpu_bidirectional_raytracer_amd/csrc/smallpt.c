@@ -11,7 +11,8 @@
  * light pass (UpdateRendering2) and then path passes; N passes are fused into launches of B.
  * KEYS replays KeyFunc/SpecialFunc: a d w s r f (camera moves), ' ' (re-init), + - (select
  * sphere), 4 6 8 2 9 3 (move the selected sphere), U D L R (arrow keys), P/p (PageUp/Down
- * targets -> here 'P' = PageUp, 'Q' = PageDown); after each key N more passes are rendered.
+ * targets -> here 'P' = PageUp, 'Q' = PageDown), p (SavePPM with the reference's file name);
+ * after each key N more passes are rendered.  --p6 writes --out as binary P6.
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -92,8 +93,30 @@ static void reinit_scene(host *h)
     update_rendering2(h);
 }
 
+/* SavePPM smallpt_cpu.c:238-262 ('p' in KeyFunc): reference file name, ASCII P3 */
+static int save_ppm(host *h, const char *path, int binary)
+{
+    char name[64];
+    if (!path) {
+        bdpt_ppm_name(name, (int)sizeof name, h->total_time, h->current_sample);
+        path = name;
+    }
+    unsigned char *rgba = malloc(4 * (size_t)h->width * h->height);
+    int rc = rgba ? bdpt_read_pixels(h->ctx, rgba) : BDPT_ENOMEM;
+    if (rc == BDPT_OK)
+        rc = binary ? bdpt_save_ppm_binary(path, rgba, h->width, h->height)
+                    : bdpt_save_ppm(path, rgba, h->width, h->height);
+    report(h, rc, "SavePPM");
+    free(rgba);
+    return rc;
+}
+
 static void key(host *h, int k)
 {
+    if (k == 'p') {
+        (void)save_ppm(h, NULL, 0);
+        return;
+    }
     int code = k;
     if (k == 'U') code = BDPT_KEY_UP;
     else if (k == 'D') code = BDPT_KEY_DOWN;
@@ -119,7 +142,7 @@ int main(int argc, char **argv)
 {
     host h;
     memset(&h, 0, sizeof(h));
-    int spp = 16, batch = 64, device = 0, npos = 0;
+    int spp = 16, batch = 64, device = 0, npos = 0, p6 = 0;
     const char *pos[3] = {0, 0, 0}, *out = NULL, *keys = "", *dat = "assets/data/MersenneTwister.dat";
     for (int a = 1; a < argc; a++) {
         if (!strcmp(argv[a], "--spp") && a + 1 < argc) spp = atoi(argv[++a]);
@@ -128,6 +151,7 @@ int main(int argc, char **argv)
         else if (!strcmp(argv[a], "--out") && a + 1 < argc) out = argv[++a];
         else if (!strcmp(argv[a], "--device") && a + 1 < argc) device = atoi(argv[++a]);
         else if (!strcmp(argv[a], "--dat") && a + 1 < argc) dat = argv[++a];
+        else if (!strcmp(argv[a], "--p6")) p6 = 1;
         else if (npos < 3) pos[npos++] = argv[a];
         else { fprintf(stderr, "Usage: %s <window width> <window height> <scene file>\n", argv[0]); return -1; }
     }
@@ -169,13 +193,7 @@ int main(int argc, char **argv)
         for (int done = 0; done < spp; done += batch)
             update_rendering(&h, spp - done < batch ? spp - done : batch);
     }
-    if (out) {                                            /* SavePPM smallpt_cpu.c:239 */
-        unsigned char *rgba = malloc(4 * (size_t)h.width * h.height);
-        rc = bdpt_read_pixels(h.ctx, rgba);
-        if (rc == BDPT_OK) rc = bdpt_save_ppm(out, rgba, h.width, h.height);
-        report(&h, rc, "SavePPM");
-        free(rgba);
-    }
+    if (out) rc = save_ppm(&h, out, p6);
     bdpt_destroy(h.ctx);
     if (npos == 3) bdpt_free_scene(h.spheres); else free(h.spheres);
     return rc == BDPT_OK ? 0 : 1;

@@ -80,6 +80,17 @@ int  bdpt_set_shard(bdpt_ctx *ctx, int shard, int nshards, int band_rows);
 int  bdpt_set_streams(bdpt_ctx *ctx, int streams);
 /* S used by the last bdpt_path_passes call. */
 int  bdpt_last_streams(const bdpt_ctx *ctx);
+/* Sphere traversal (no reference counterpart; results are bit-identical either way).  The
+ * reference tests every sphere per ray (IntersectDevice device.cu:106-124); for scenes with
+ * > 16 spheres of which >= 24 are of ordinary size, bdpt_set_scene also builds a BVH over those
+ * (walls stay brute force) that skips only spheres that provably cannot change the answer. */
+#define BDPT_TRAVERSE_AUTO  0               /* BVH when the scene has one                    */
+#define BDPT_TRAVERSE_BRUTE 1               /* every sphere, like the reference             */
+#define BDPT_TRAVERSE_BVH   2               /* same as AUTO                                  */
+int  bdpt_set_traversal(bdpt_ctx *ctx, int mode);
+int  bdpt_scene_has_bvh(const bdpt_ctx *ctx);
+/* BDPT_TRAVERSE_BVH or BDPT_TRAVERSE_BRUTE: what the last bdpt_path_passes call used. */
+int  bdpt_last_traversal(const bdpt_ctx *ctx);
 
 /* UpdateRendering2 smallpt_cpu.c:300-362: for every emitter in sphere order,
  * seedMTGPU(current_sample*5) + RandomGPU (MT607 table), GetRayKernel and
@@ -135,6 +146,10 @@ int  bdpt_camera_key(bdpt_camera *camera, int key);
 int  bdpt_sphere_key(bdpt_sphere *spheres, unsigned n_spheres, int current_sphere, int key);
 /* SavePPM smallpt_cpu.c:239-262: ASCII P3, rows written bottom-up. */
 int  bdpt_save_ppm(const char *path, const unsigned char *rgba, int width, int height);
+/* Binary P6 with the same header numbers and bottom-up rows (no reference counterpart). */
+int  bdpt_save_ppm_binary(const char *path, const unsigned char *rgba, int width, int height);
+/* SavePPM file name smallpt_cpu.c:245, "max1_secondi%.3f_exe%d.ppm", bounded by `size`. */
+int  bdpt_ppm_name(char *buf, int size, float total_time, int current_sample);
 /* The 256 thresholds behind the kernel's toInt (vec.h:34): thr[k] = smallest float whose
  * toInt is >= k (thr[0] = -inf), with correctly-rounded powf semantics. */
 void bdpt_gamma_thresholds(float thr[256]);

@@ -115,3 +115,19 @@ class Session:
     def SpecialFunc(self, key: str):
         if special_key(self.camera, key):
             self.ReInit(1)
+
+
+def save_ppm_text(pixels: np.ndarray) -> str:
+    """SavePPM file body (smallpt_cpu.c:247-258): "P3\\n%d %d\\n%d\\n", then rows from y = H-1
+    down to 0, "%d %d %d " per pixel (R, G, B of the uchar4)."""
+    h, w = pixels.shape[:2]
+    parts = ["P3\n%d %d\n%d\n" % (w, h, 255)]
+    for y in range(h - 1, -1, -1):
+        parts.append("".join("%d %d %d " % (int(p[0]), int(p[1]), int(p[2])) for p in pixels[y]))
+    return "".join(parts)
+
+
+def ppm_name(total_time: float, current_sample: int) -> str:
+    """smallpt_cpu.c:245 sprintf(name, "max%d_secondi%.3f_exe%d.ppm", MAX_VLP, total_time, ...)
+    with the float total_time promoted to double by the varargs call."""
+    return "max%d_secondi%.3f_exe%d.ppm" % (MAX_VLP, float(np.float32(total_time)), current_sample)

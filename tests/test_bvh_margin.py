@@ -1,0 +1,95 @@
+"""The BVH's culling margin must cover the float error of the reference's sphere test.
+
+SphereIntersectDevice (device.cu:80-104): op = p-o, b = op.d, det = b*b - op.op + r*r,
+t = b -+ sqrt(det) accepted if > 0.01.  The BVH (bdpt_kernels.hip bvh_setup/bvh_box) skips a
+box only if the ray enters it beyond tmax + m or leaves it before -m, where the box is widened
+by the per-ray margin m = D*(4e-3 + q*D), D >= |op| + r, q = 32u / r_min.  That is exact iff
+every float hit point X = o + t*d lies inside its sphere's bounding box widened by m.  Checked
+here, with 2x slack (m/2), on 3M rays aimed at the worst cases -- tangent and near-tangent rays
+where det cancels, tiny spheres far away where the non-unit float direction matters -- using
+numpy float32 (IEEE, no contraction) for the test and long double for the geometry."""
+import numpy as np
+
+K, U = 4e-3, 2.0 ** -24
+
+
+def _float_test(p, rr, o, d):
+    f = np.float32
+    op = (p - o).astype(f)
+    b = (op[:, 0] * d[:, 0] + op[:, 1] * d[:, 1]) + op[:, 2] * d[:, 2]
+    oo = (op[:, 0] * op[:, 0] + op[:, 1] * op[:, 1]) + op[:, 2] * op[:, 2]
+    det = (b * b - oo) + rr
+    ok = det >= 0
+    s = np.sqrt(np.where(ok, det, f(0)))
+    t1, t2 = b - s, b + s
+    t = np.where(t1 > f(0.01), t1, t2)
+    return ok & (t > f(0.01)), t
+
+
+def _rays(rng, n, radii, dmax):
+    f = np.float32
+    r = rng.choice(np.array(radii, f), n)
+    p = rng.uniform(-50, 100, (n, 3)).astype(f)
+    dist = np.exp(rng.uniform(np.log(1.0), np.log(dmax), n))
+    u = rng.normal(size=(n, 3))
+    u /= np.linalg.norm(u, axis=1, keepdims=True)
+    o = (p + u * dist[:, None]).astype(f)
+    w = rng.normal(size=(n, 3))
+    w -= (w * u).sum(1, keepdims=True) * u
+    w /= np.linalg.norm(w, axis=1, keepdims=True)
+    e = rng.choice(np.array([0.0, 1e-7, -1e-7, 1e-5, -1e-5, 1e-3, -1e-3, 0.3, -0.5]), n)
+    v = (p + w * (r * (1 + e))[:, None] - o).astype(f)     # aim at / near the silhouette
+    d = (v * (f(1) / np.sqrt((v * v).sum(1)).astype(f))[:, None]).astype(f)   # float vnorm
+    return p, r, o, d
+
+
+def _check(p, r, o, d):
+    rr = (r * r).astype(np.float32)
+    hit, t = _float_test(p, rr, o, d)
+    L = np.longdouble
+    X = o[hit].astype(L) + t[hit].astype(L)[:, None] * d[hit].astype(L)
+    c, rad = p[hit].astype(L), r[hit].astype(L)
+    outside = np.maximum(np.abs(X - c) - rad[:, None], 0).max(1)       # Chebyshev gap to the box
+    D = np.sqrt(((p[hit].astype(L) - o[hit].astype(L)) ** 2).sum(1)) + rad
+    m = D * (K + 32 * U / rad * D)
+    return hit, float((outside / m).max())
+
+
+def test_float_hits_lie_within_half_margin():
+    rng = np.random.default_rng(11)
+    # the large scenes' radii at their distances
+    hit, worst = _check(*_rays(rng, 2_000_000, [0.9375, 1.875, 3.75, 7.5, 15.0], 400.0))
+    assert hit.sum() > 500_000
+    assert worst < 0.5, worst
+    # tiny spheres seen from far away (D/r up to 5e4): the q*D^2 term
+    hit, worst = _check(*_rays(rng, 1_000_000, [0.01, 0.1, 0.5], 5000.0))
+    assert hit.sum() > 200_000
+    assert worst < 0.5, worst
+
+
+def test_bvh_traversal_matches_brute_force_on_cpu(tmp_path):
+    """tests/native/bvh_check.cpp: the real tree builder + the kernel's traversal restated on the
+    host, against the every-sphere loops, on 100k camera/bounce/shadow rays per scene."""
+    import json
+    import os
+    import subprocess
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    hipcc = "/opt/rocm/bin/hipcc"
+    flags = ["-O2", "-fPIC", "-ffp-contract=off", "-std=c++17"]
+    objs = []
+    for src in ("tests/native/bvh_check.cpp", "gpu_bidirectional_raytracer_amd/csrc/bdpt_bvh.cpp"):
+        obj = str(tmp_path / (os.path.basename(src) + ".o"))
+        subprocess.check_call([hipcc, *flags, "-c", os.path.join(repo, src), "-o", obj])
+        objs.append(obj)
+    util = str(tmp_path / "bdpt_util.o")
+    subprocess.check_call(["gcc", "-O2", "-fPIC", "-ffp-contract=off", "-c",
+                           os.path.join(repo, "gpu_bidirectional_raytracer_amd/csrc/bdpt_util.c"), "-o", util])
+    exe = str(tmp_path / "bvh_check")
+    subprocess.check_call(["g++", "-o", exe, *objs, util, "-lm"])
+    for scene in ("complex", "mod_cornell", "synthetic64"):
+        out = subprocess.run([exe, os.path.join(repo, "assets", "scenes", scene + ".scn"), "100000", "5"],
+                             capture_output=True, text=True)
+        rec = json.loads(out.stdout)
+        assert out.returncode == 0 and rec["bvh"], (scene, out.stdout, out.stderr)
+        assert rec["bad_closest"] == 0 and rec["bad_shadow"] == 0, rec
+        assert rec["sphere_tests_per_ray"] < 40, rec                 # vs 58..789 brute force

@@ -321,3 +321,60 @@ def test_rccl_frame_assembly_world1(gpu):
     finally:
         dist.destroy_process_group()
         r.close()
+
+
+# ---- large scenes through the BVH (bdpt_bvh.cpp) --------------------------------
+@pytest.mark.parametrize("name,W,H,npass", [("complex", 64, 48, 4), ("mod_cornell", 48, 36, 4),
+                                            ("synthetic64", 40, 30, 4)])
+def test_bvh_bit_exact_vs_oracle(gpu, rnd0, name, W, H, npass):
+    r, cam, sp = make(name, W, H, gpu)
+    assert r.has_bvh
+    sid, vlp = schedule(npass)
+    r.path_passes(sid, vlp)
+    assert r.last_traversal == "bvh"
+    col, cnt = r.read_radiance()
+    lp = oracle.light_pass(sp, rnd0, 0)
+    ocol, ocnt, opix = oracle.path_passes(sp, rnd0, cam, W, H, lp, sid, vlp)
+    assert_same(cnt, ocnt, "counter")
+    assert_same(col, ocol, "colors")
+    assert_same(r.read_pixels(), opix, "pixels")
+    r.close()
+
+
+@pytest.mark.parametrize("name,keys", [("mod_cornell", ""), ("complex", ""), ("mod_cornell", "s" * 40),
+                                       ("complex", "s" * 60 + "r" * 10)])
+def test_bvh_equals_brute_force(gpu, name, keys):
+    """Same frame through the BVH and through the reference's every-sphere loop, bit for bit;
+    the camera moved far back (tiny spheres at long range: the margin's q*D^2 term)."""
+    W, H = 241, 181
+    sid, vlp = schedule(3)
+    out = []
+    for mode in ("bvh", "brute"):
+        cam, sp = scene(name)
+        g.update_camera(cam, W, H)
+        for k in keys:
+            g.camera_key(cam, k)
+            g.update_camera(cam, W, H)
+        r = g.Renderer(sp, W, H, cam, device=gpu)
+        r.light_pass(0)
+        r.set_traversal(mode)
+        r.path_passes(sid, vlp)
+        assert r.last_traversal == mode
+        out.append(r.read_radiance())
+        r.close()
+    assert_same(out[0][1], out[1][1], "counter")
+    assert_same(out[0][0], out[1][0], "colors")
+
+
+def test_bvh_1080p_oracle_rows(gpu, rnd0):
+    W, H = 1921, 1081
+    r, cam, sp = make("mod_cornell", W, H, gpu)
+    sid, vlp = schedule(2)
+    r.path_passes(sid, vlp)
+    col, cnt = r.read_radiance()
+    assert (cnt == 2).all()
+    lp = oracle.light_pass(sp, rnd0, 0)
+    for y in (0, 333, 1080):
+        ocol, _, _ = oracle.path_passes(sp, rnd0, cam, W, H, lp, sid, vlp, rows=(y, y + 1))
+        assert_same(col[y], ocol[y], f"row {y}")
+    r.close()

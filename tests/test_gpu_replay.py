@@ -92,3 +92,23 @@ def test_smallpt_host_keys_match_oracle(gpu, tmp_path):
         for _ in range(3):
             ora.IdleFunc()
     _same(_read_ppm(out), ora.pixels[..., :3].astype(np.int64), "smallpt --keys PPM")
+
+
+def test_smallpt_save_key_and_p6(gpu, tmp_path):
+    """'p' saves with the reference's name pattern (P3, the pixels at that moment); --p6 writes
+    the same image as binary P6 (two deterministic runs of one configuration)."""
+    exe = os.path.join(REPO, "gpu_bidirectional_raytracer_amd", "smallpt")
+    base = [exe, "16", "12", os.path.join(SCENES, "caustic.scn"), "--spp", "2", "--dat", DAT]
+    quiet = dict(cwd=tmp_path, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    subprocess.check_call(base + ["--keys", "p", "--out", str(tmp_path / "after.ppm")], **quiet)
+    saved = [f for f in os.listdir(tmp_path) if f.startswith("max1_secondi")]
+    assert len(saved) == 1 and saved[0].endswith("_exe2.ppm"), saved
+    subprocess.check_call(base + ["--out", str(tmp_path / "a.ppm")], **quiet)
+    subprocess.check_call(base + ["--out", str(tmp_path / "b.ppm"), "--p6"], **quiet)
+    p3 = _read_ppm(tmp_path / "a.ppm")
+    assert np.array_equal(_read_ppm(tmp_path / saved[0]), p3)   # 'p' saw 2 passes too
+    raw = (tmp_path / "b.ppm").read_bytes()
+    head = b"P6\n17 13\n255\n"
+    assert raw.startswith(head)
+    p6 = np.frombuffer(raw[len(head):], np.uint8).reshape(13, 17, 3)[::-1]
+    assert np.array_equal(p3, p6.astype(np.int64))

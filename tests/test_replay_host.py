@@ -69,3 +69,19 @@ def test_host_vnorm_is_c_double_sqrt():
     dd = np.float32(d[0] * d[0] + d[1] * d[1]) + np.float32(d[2] * d[2])
     lc = np.float32(1.0 / np.sqrt(np.float64(dd)))
     np.testing.assert_array_equal(_vec(cam.dir), lc * d)
+
+
+def test_save_ppm_matches_oracle(tmp_path):
+    from oracle.replay import ppm_name, save_ppm_text
+    rng = np.random.default_rng(3)
+    for h, w in ((1, 1), (7, 5), (25, 33)):
+        px = rng.integers(0, 256, (h, w, 4), dtype=np.uint8)
+        g.save_ppm(str(tmp_path / "a.ppm"), px)
+        assert (tmp_path / "a.ppm").read_text() == save_ppm_text(px)
+        g.save_ppm(str(tmp_path / "b.ppm"), px, binary=True)
+        raw = (tmp_path / "b.ppm").read_bytes()
+        head = b"P6\n%d %d\n255\n" % (w, h)
+        assert raw[:len(head)] == head
+        assert raw[len(head):] == px[::-1, :, :3].tobytes()
+    for t, n in ((0.0, 0), (1.23456, 17), (999.9996, 1024), (12345.678, 8192)):
+        assert g.ppm_name(t, n) == ppm_name(t, n)
