@@ -197,6 +197,9 @@ def main():
                     "flop_per_sample": round(flop_per_sample(w), 1),
                     "note": "bound: fp32 VALU (no contraction, correctly rounded div/sqrt); "
                             "FLOP model in DESIGN.md"}
+            if r.last_traversal == "bvh":
+                valu["note"] = ("reference-equivalent FLOPs: the reference tests every sphere; the BVH "
+                                "skips most tests, so this is work avoided, not VALU throughput")
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(sp, cam, W, H, sid, vlp, args.cpu_seconds)

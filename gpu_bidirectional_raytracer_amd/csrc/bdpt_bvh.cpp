@@ -136,7 +136,7 @@ bool bdpt_build_bvh(const bdpt_sphere* s, unsigned n, bdpt_bvh* out) {
         rmin = std::min(rmin, std::min(std::fabs((double)s[j].rad),
                                        std::sqrt((double)(s[j].rad * s[j].rad))) * (1.0 - 1e-6));
     }
-    out->q = rmin > 0.0 ? (float)(32.0 * 0x1p-24 / rmin * (1.0 + 1e-6)) : INFINITY;
+    out->q = rmin > 0.0 ? (float)(64.0 * 0x1p-24 / rmin * (1.0 + 1e-6)) : INFINITY;
     for (const item& t : it) {
         const int i = t.id & ~kBvhEmissive;
         const double dx = s[i].p.x - c[0], dy = s[i].p.y - c[1], dz = s[i].p.z - c[2];

@@ -9,8 +9,19 @@
 
 #include "../../include/bdpt.h"
 
-constexpr int kBvhLeaf = 4;              // spheres per leaf
-constexpr int kBvhMinSpheres = 24;       // fewer BVH spheres: brute force is as fast
+#ifndef BDPT_BVH_LEAF
+#define BDPT_BVH_LEAF 4
+#endif
+#ifndef BDPT_BVH_MIN
+#define BDPT_BVH_MIN 24
+#endif
+#ifndef BDPT_BVH_AUTO
+#define BDPT_BVH_AUTO 128
+#endif
+constexpr int kBvhLeaf = BDPT_BVH_LEAF;          // spheres per leaf
+constexpr int kBvhMinSpheres = BDPT_BVH_MIN;     // fewer BVH spheres: no tree
+constexpr int kBvhAutoSpheres = BDPT_BVH_AUTO;   // auto mode: fewer -> brute force (faster on
+                                                 // synthetic64's 58, measured)
 constexpr int kBvhEmissive = 1 << 30;    // id flag: emissive (IntersectPVacuum skips it)
 
 struct bdpt_bvh {
@@ -22,7 +33,7 @@ struct bdpt_bvh {
     std::vector<int> big_ids;
     float c_root[3] = {0.f, 0.f, 0.f};   // every BVH sphere lies inside the ball (c_root, r_root)
     float r_root = 0.f;
-    float q = 0.f;                       // 32 * 2^-24 / smallest BVH sphere radius
+    float q = 0.f;                       // 64 * 2^-24 / smallest BVH sphere radius
 };
 
 // host-side reinterpretation of int bits as a float (node / table packing)

@@ -80,7 +80,7 @@ struct bdpt_path_args {
     const float4* mat;              // per sphere: {c, refl | emissive<<8}, {e, rad}, {p, 0}
     int bvh_nn, bvh_ns, big_n;
     float bvh_c[3], bvh_r;          // ball around every BVH sphere (per-ray margin)
-    float bvh_q;                    // 32u / smallest BVH radius (per-ray margin)
+    float bvh_q;                    // 64u / smallest BVH radius (per-ray margin)
 };
 
 // Tile row of a workgroup row: identity, or the sub-th tile row of this shard's k-th band.

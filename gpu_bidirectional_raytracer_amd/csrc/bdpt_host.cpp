@@ -468,7 +468,8 @@ int bdpt_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int npass
     if (S < 1) S = 1;
     a.streams = S;
     c->last_streams = S;
-    const bool bvh = c->has_bvh && c->traversal != BDPT_TRAVERSE_BRUTE;
+    const bool bvh = c->has_bvh && (c->traversal == BDPT_TRAVERSE_BVH ||
+                                    (c->traversal == BDPT_TRAVERSE_AUTO && c->bvh_ns >= kBvhAutoSpheres));
     const void* kern = bdpt_path_kernel_table[(S > 1) * 18 + (bvh ? 17 : (a.n <= 16 ? a.n : 0))];
     if (bvh) {
         a.bvh_nodes = c->d_bvh_nodes; a.bvh_geom = c->d_bvh_geom; a.bvh_ids = c->d_bvh_ids;

@@ -257,16 +257,20 @@ __device__ __forceinline__ void wave_lds_fence() {
 }
 
 // ---- BVH traversal (large scenes; tree built by bdpt_bvh.cpp) --------------------------------
-// The float sphere test (SphereIntersectDevice) differs from the exact root of its own formula
-// by at most ~sqrt(20u)*(|op|+r) ~ 1.1e-3*(|op|+r) (u = 2^-24; the det cancellation under the
-// sqrt dominates), and a float hit on an exactly-missed sphere lies within the same distance of
-// it.  The float direction is unit only to ~8u, which acts like a radius error of ~8u*D^2/r.
-// Every box is therefore widened by m = D*(kBvhK + q*D), D = |o - c_root| + r_root >= |op|+r
-// for all BVH spheres, q = 32u / (smallest BVH radius) -- 3.6x and 4x those bounds;
-// tests/test_bvh_margin.py checks on worst-case rays that every float hit point lies within
-// m/2 of its sphere's box -- and a box is skipped only if entered beyond tmax + m or left
-// before -m.
-constexpr float kBvhK = 4e-3f;
+// Exactness: a box may be skipped only if no sphere in it can produce a float hit that changes
+// the answer.  For the reference's float test t^ = fl(b -+ sqrt(det)) (SphereIntersectDevice),
+// with g(t) = |o + t d - p|^2 - r^2 on the same float inputs, expanding g(t^) around the float
+// det gives |g(t^)| <= ~50u D^2 (u = 2^-24; det rounding, sqrt rounding, the b error times
+// sqrt(det), and |d|^2 - 1 = O(u) from the float vnorm), D >= |op| + r.  So every float hit
+// point -- also on an exactly-missed sphere -- lies within 25u D^2 / r of its sphere, hence of
+// its box.  Boxes are widened by m = D*(kBvhK + q*D), q = 64u / (smallest BVH radius) (2.6x
+// that bound) and kBvhK = 1e-4 (covers the slab test's own ~6u*D rounding ~270x), with
+// D = |o - c_root| + r_root; a box is skipped only if entered beyond tmax + m or left before
+// -m.  tests/test_bvh_margin.py measures the gap on worst-case rays against m/2.
+#ifndef BDPT_BVH_K
+#define BDPT_BVH_K 1e-4f
+#endif
+constexpr float kBvhK = BDPT_BVH_K;
 constexpr int kBvhEmissive = BDPT_DEV_BVH_EMISSIVE;
 constexpr int kBvhIdMask = BDPT_DEV_BVH_EMISSIVE - 1;
 
@@ -446,18 +450,23 @@ __global__ __launch_bounds__(256, N < 0 ? 4 : BDPT_WAVES_PER_SIMD) void bdpt_pat
                 }
                 const bvh_ray br = bvh_setup(a, ro, rd);
                 int node = 0;
-                while (node < a.bvh_nn) {
-                    const float4 lo = ND[2 * node], hi = ND[2 * node + 1];
-                    const int info = __float_as_int(hi.w);
-                    if (!bvh_box(lo, hi, br, t)) { node = __float_as_int(lo.w); continue; }
-                    if (info < 0) { node++; continue; }
+                // while-while: walk inner nodes until this lane has a leaf, then test leaves
+                while (true) {
+                    int info = -1;
+                    while (node < a.bvh_nn) {
+                        const float4 lo = ND[2 * node], hi = ND[2 * node + 1];
+                        const int inf = __float_as_int(hi.w);
+                        const bool in = bvh_box(lo, hi, br, t);
+                        node = (in && inf < 0) ? node + 1 : __float_as_int(lo.w);
+                        if (in && inf >= 0) { info = inf; break; }
+                    }
+                    if (info < 0) break;
                     const int first = info & 0xffffff, end = first + (info >> 24);
                     for (int k = first; k < end; k++) {
                         const float d = sphere_isect_inf(SG[k], ro, rd);
                         const int s = SI[k] & kBvhIdMask;
                         if (d < t || (d == t && s > id)) { t = d; id = s; }
                     }
-                    node = __float_as_int(lo.w);
                 }
             } else {
 #pragma unroll kUnroll

@@ -84,9 +84,9 @@ int  bdpt_last_streams(const bdpt_ctx *ctx);
  * reference tests every sphere per ray (IntersectDevice device.cu:106-124); for scenes with
  * > 16 spheres of which >= 24 are of ordinary size, bdpt_set_scene also builds a BVH over those
  * (walls stay brute force) that skips only spheres that provably cannot change the answer. */
-#define BDPT_TRAVERSE_AUTO  0               /* BVH when the scene has one                    */
+#define BDPT_TRAVERSE_AUTO  0               /* BVH when it has >= 128 spheres                */
 #define BDPT_TRAVERSE_BRUTE 1               /* every sphere, like the reference             */
-#define BDPT_TRAVERSE_BVH   2               /* same as AUTO                                  */
+#define BDPT_TRAVERSE_BVH   2               /* BVH whenever the scene has one               */
 int  bdpt_set_traversal(bdpt_ctx *ctx, int mode);
 int  bdpt_scene_has_bvh(const bdpt_ctx *ctx);
 /* BDPT_TRAVERSE_BVH or BDPT_TRAVERSE_BRUTE: what the last bdpt_path_passes call used. */

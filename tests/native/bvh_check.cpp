@@ -37,7 +37,7 @@ bvh_ray setup(const bdpt_bvh& B, v3 o, v3 d) {
     const v3 dc = sub(o, {B.c_root[0], B.c_root[1], B.c_root[2]});
     const float D = sqrtf(dot(dc, dc) * 1.00001f) * 1.00001f + B.r_root;
     bvh_ray r;
-    r.m = D * (4e-3f + B.q * D);
+    r.m = D * (1e-4f + B.q * D);
     r.olo = {o.x + r.m, o.y + r.m, o.z + r.m};
     r.ohi = {o.x - r.m, o.y - r.m, o.z - r.m};
     const float e = 1e-20f;

@@ -3,14 +3,14 @@
 SphereIntersectDevice (device.cu:80-104): op = p-o, b = op.d, det = b*b - op.op + r*r,
 t = b -+ sqrt(det) accepted if > 0.01.  The BVH (bdpt_kernels.hip bvh_setup/bvh_box) skips a
 box only if the ray enters it beyond tmax + m or leaves it before -m, where the box is widened
-by the per-ray margin m = D*(4e-3 + q*D), D >= |op| + r, q = 32u / r_min.  That is exact iff
+by the per-ray margin m = D*(1e-4 + q*D), D >= |op| + r, q = 64u / r_min.  That is exact iff
 every float hit point X = o + t*d lies inside its sphere's bounding box widened by m.  Checked
 here, with 2x slack (m/2), on 3M rays aimed at the worst cases -- tangent and near-tangent rays
 where det cancels, tiny spheres far away where the non-unit float direction matters -- using
 numpy float32 (IEEE, no contraction) for the test and long double for the geometry."""
 import numpy as np
 
-K, U = 4e-3, 2.0 ** -24
+K, U = 1e-4, 2.0 ** -24
 
 
 def _float_test(p, rr, o, d):
@@ -51,7 +51,7 @@ def _check(p, r, o, d):
     c, rad = p[hit].astype(L), r[hit].astype(L)
     outside = np.maximum(np.abs(X - c) - rad[:, None], 0).max(1)       # Chebyshev gap to the box
     D = np.sqrt(((p[hit].astype(L) - o[hit].astype(L)) ** 2).sum(1)) + rad
-    m = D * (K + 32 * U / rad * D)
+    m = D * (K + 64 * U / rad * D)
     return hit, float((outside / m).max())
 
 

@@ -329,6 +329,7 @@ def test_rccl_frame_assembly_world1(gpu):
 def test_bvh_bit_exact_vs_oracle(gpu, rnd0, name, W, H, npass):
     r, cam, sp = make(name, W, H, gpu)
     assert r.has_bvh
+    r.set_traversal("bvh")                    # synthetic64 (58 BVH spheres) is brute force in auto
     sid, vlp = schedule(npass)
     r.path_passes(sid, vlp)
     assert r.last_traversal == "bvh"
