@@ -47,6 +47,16 @@ for s in $STEPS; do
   shard)
     timeout -k 10 400 python scripts/shard_probe.py ${SHARD_ARGS:-} > gpurun_out/shard_probe.log 2>&1
     rc=$?; cat gpurun_out/shard_probe.log | tail -12; ok_or_stop $rc shard ;;
+  calib)
+    # FETCH_SIZE / WRITE_SIZE calibration on known byte counts (scripts/pmc_calib.hip)
+    [ -x scripts/pmc_calib ] || /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -o scripts/pmc_calib scripts/pmc_calib.hip
+    for c in FETCH_SIZE WRITE_SIZE; do
+      rm -rf gpurun_out/calib_$c
+      timeout -k 10 180 rocprofv3 --pmc $c --kernel-trace -d gpurun_out/calib_$c -o run --output-format csv -- \
+          ./scripts/pmc_calib > gpurun_out/calib_$c.log 2>&1
+      rc=$?; echo "calib $c rc=$rc"; ok_or_stop $rc calib_$c
+    done
+    cp gpurun_out/calib_FETCH_SIZE.log gpurun_out/calib_bytes.jsonl ;;
   pmc)
     rocprofv3 -L > gpurun_out/counters_list.txt 2>&1 || true
     i=0

@@ -1,24 +1,61 @@
-"""Write profiles/pmc_traffic.json from a `STEPS=pmc` run (gpurun_out/pmc*/): FETCH_SIZE and
-WRITE_SIZE (KiB, separate passes) of the path kernel, averaged over its dispatches.
-Caveats (MI355X_MICROARCH.md "HBM"): both count L2<->fabric traffic, so Infinity-Cache hits are
-included (the 30.7 MB RNG table lives there); FETCH_SIZE is calibrated only for 16-B/lane streams
-(the path kernel gathers dwords), so the figure is an upper-level traffic estimate."""
+"""Write profiles/pmc_traffic.json from a `STEPS="calib pmc"` run (gpurun_out/): FETCH_SIZE and
+WRITE_SIZE (KiB, separate --pmc passes) of the path kernel, averaged over its dispatches, and
+corrected as MI355X_MICROARCH.md "HBM" prescribes: FETCH_SIZE under-reports wide reads on gfx950
+(1/2 for 16-B/lane streams) and other access widths must be calibrated on a known byte count in
+the kernel's own access pattern -- scripts/pmc_calib.hip measures the counters on 1 GiB of
+16-B streams, 20-B-per-128-B-line gathers (the RNG prefetch), 12-B AoS reads (colors) and 4-B /
+12-B stores.  The path kernel's reads are dominated by the gathers, so its FETCH_SIZE is scaled
+by line_bytes / FETCH(gather20): HBM bytes at 128-B line granularity, an upper estimate (the
+counters include Infinity-Cache hits; the 30.7 MB table lives there)."""
 import csv, glob, json, os, sys
 
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
 out = sys.argv[2] if len(sys.argv) > 2 else "profiles/pmc_traffic.json"
-vals = {}
-for f in glob.glob(os.path.join(root, "pmc*", "run_counter_collection.csv")):
-    for r in csv.DictReader(open(f)):
-        if "path_kernel" in r["Kernel_Name"] and r["Counter_Name"] in ("FETCH_SIZE", "WRITE_SIZE"):
-            vals.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
-fetch = sum(vals["FETCH_SIZE"]) / len(vals["FETCH_SIZE"]) * 1024
-write = sum(vals["WRITE_SIZE"]) / len(vals["WRITE_SIZE"]) * 1024
+
+
+def counter(pattern, kernel, name):
+    vals = []
+    for f in glob.glob(os.path.join(root, pattern, "run_counter_collection.csv")):
+        for r in csv.DictReader(open(f)):
+            if kernel in r["Kernel_Name"] and r["Counter_Name"] == name:
+                vals.append(float(r["Counter_Value"]) * 1024)
+    return sum(vals) / len(vals) if vals else None, len(vals)
+
+
+fetch, nd = counter("pmc*", "path_kernel", "FETCH_SIZE")
+write, _ = counter("pmc*", "path_kernel", "WRITE_SIZE")
+known = {}
+kb = os.path.join(root, "calib_bytes.jsonl")
+if os.path.exists(kb):
+    for line in open(kb):
+        if line.startswith("{"):
+            d = json.loads(line)
+            known[d["kernel"]] = d
+calib = {}
+for k, d in known.items():
+    if "read_bytes" in d:
+        v, _ = counter("calib_FETCH_SIZE", k, "FETCH_SIZE")
+        calib[k] = {"fetch_reported": v, **{x: d[x] for x in d if x != "kernel"}}
+    if "write_bytes" in d:
+        v, _ = counter("calib_WRITE_SIZE", k, "WRITE_SIZE")
+        calib[k] = {"write_reported": v, **{x: d[x] for x in d if x != "kernel"}}
+for k, c in calib.items():
+    if c.get("fetch_reported"):
+        c["read_bytes_per_reported"] = round(c["read_bytes"] / c["fetch_reported"], 4)
+        if "line_bytes" in c:
+            c["line_bytes_per_reported"] = round(c["line_bytes"] / c["fetch_reported"], 4)
+    if c.get("write_reported"):
+        c["write_bytes_per_reported"] = round(c["write_bytes"] / c["write_reported"], 4)
+fscale = calib.get("gather20", {}).get("line_bytes_per_reported")
+wscale = calib.get("store12", {}).get("write_bytes_per_reported")
 rec = {"scene": "cornell", "width": 1921, "height": 1081, "passes_per_launch": 16.0,
-       "fetch_bytes_per_launch": int(fetch), "write_bytes_per_launch": int(write),
-       "hbm_bytes_per_launch": int(fetch + write), "dispatches": len(vals["FETCH_SIZE"]),
-       "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), x1024",
-       "caveat": __doc__.split("Caveats", 1)[1].strip()}
+       "fetch_reported_bytes_per_launch": int(fetch), "write_reported_bytes_per_launch": int(write),
+       "fetch_scale": fscale, "write_scale": wscale,
+       "hbm_bytes_per_launch": int(fetch * (fscale or 1.0) + write * (wscale or 1.0)),
+       "dispatches": nd, "calibration": calib,
+       "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), x1024, calibrated",
+       "method": __doc__}
 os.makedirs(os.path.dirname(out), exist_ok=True)
 json.dump(rec, open(out, "w"), indent=1)
-print(json.dumps(rec))
+print(json.dumps({k: v for k, v in rec.items() if k not in ("method", "calibration")}))
+print(json.dumps(calib))
