@@ -88,7 +88,7 @@ def main():
     ap.add_argument("--scene", default="cornell")
     ap.add_argument("--width", type=int, default=1920, help="CLI width (internal = +1)")
     ap.add_argument("--height", type=int, default=1080, help="CLI height (internal = +1)")
-    ap.add_argument("--passes", type=int, default=16, help="passes per step per GPU share")
+    ap.add_argument("--passes", type=int, default=32, help="passes per step per GPU share")
     ap.add_argument("--band-rows", type=int, default=8)
     ap.add_argument("--traversal", default="auto", choices=["auto", "brute", "bvh"],
                     help="sphere traversal for >16-sphere scenes (results identical)")
@@ -159,7 +159,8 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
 
-    dev_ms, launches = r.path_timing()
+    kern_ms, _ = r.kernel_timing()                            # path kernels alone
+    dev_ms, launches = r.path_timing()                        # + the pass-stream fold
     samples = W * H * per_step * args.steps                   # every pixel exactly once per pass
     value = samples / dt / 1e6
 
@@ -170,20 +171,24 @@ def main():
             assert (cnt == per_step * (args.warmup + args.steps)).all(), "reduced counters wrong"
         own_pixels = shd.owned_pixels(W, H, rank, world, args.band_rows)
         w = WORK.get(args.scene)
-        avg_launch_s = dev_ms / 1e3 / max(launches, 1)
+        avg_launch_s = kern_ms / 1e3 / max(launches, 1)
         passes_per_launch = per_step * args.steps / max(launches, 1)
         roofline = valu = None
         if w is not None:
             samples_per_launch = own_pixels * passes_per_launch
-            bytes_per_launch = own_pixels * ACCUM_BYTES_PER_PIXEL + samples_per_launch * 4 * w["rng_reads"]
-            if r.last_streams > 1:          # pass-stream radiance: 12 B written + 12 B folded
-                bytes_per_launch += samples_per_launch * 24
+            if r.last_streams > 1:
+                # pass streams: the path kernel reads the counter once and writes 12 B of radiance
+                # per sample; the fold kernel (not this launch) does the colors/pixels RMW
+                bytes_per_launch = own_pixels * 4 + samples_per_launch * (4 * w["rng_reads"] + 12)
+            else:
+                bytes_per_launch = own_pixels * ACCUM_BYTES_PER_PIXEL + samples_per_launch * 4 * w["rng_reads"]
             achieved = bytes_per_launch / avg_launch_s / 1e9
             traffic = None
             pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
             if os.path.exists(pmc):
                 rec = json.load(open(pmc))
                 if rec.get("scene") == args.scene and rec.get("passes_per_launch") == passes_per_launch \
+                        and rec.get("pass_streams") in (None, r.last_streams) \
                         and rec.get("width") == W and rec.get("height") == H and world == 1:
                     traffic = rec.get("hbm_bytes_per_launch")
             roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,

@@ -256,6 +256,12 @@ class Renderer:
         self._chk(lib.bdpt_path_timing(self._h, ctypes.byref(ms), ctypes.byref(n), int(reset)))
         return ms.value, n.value
 
+    def kernel_timing(self, reset: bool = False) -> Tuple[float, int]:
+        """(ms inside the path kernels alone, launches) since the last reset."""
+        ms, n = ctypes.c_double(), ctypes.c_longlong()
+        self._chk(lib.bdpt_kernel_timing(self._h, ctypes.byref(ms), ctypes.byref(n), int(reset)))
+        return ms.value, n.value
+
     def update_pixels(self) -> None:
         self._chk(lib.bdpt_update_pixels(self._h))
 

@@ -70,6 +70,7 @@ _SIGS = [
     ("bdpt_set_streams", ctypes.c_int, [_P, ctypes.c_int]),
     ("bdpt_last_streams", ctypes.c_int, [_P]),
     ("bdpt_set_traversal", ctypes.c_int, [_P, ctypes.c_int]),
+    ("bdpt_kernel_timing", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong), ctypes.c_int]),
     ("bdpt_scene_has_bvh", ctypes.c_int, [_P]),
     ("bdpt_last_traversal", ctypes.c_int, [_P]),
     ("bdpt_light_pass", ctypes.c_int, [_P, ctypes.c_int]),

@@ -46,6 +46,8 @@ struct bdpt_ctx {
     double acc_ms = 0.0;         // accumulated device time of finished path-pass calls
     long long acc_launches = 0;
     float last_ms = 0.f;
+    std::vector<hipEvent_t> kev;   // per path-kernel launch: {before, after} (pool, reused)
+    double acc_kernel_ms = 0.0;    // path kernels alone (no fold kernel)
     int W = 0, H = 0;
     std::vector<bdpt_sphere> spheres;
     std::vector<int> lights;
@@ -198,6 +200,7 @@ static void release(bdpt_ctx* c) {
                     c->d_bvh_geom, c->d_big_geom, c->d_mat, c->d_bvh_ids, c->d_big_ids};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
+    for (hipEvent_t e : c->kev) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -211,6 +214,11 @@ static int fold_timing(bdpt_ctx* c) {
     HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
     c->last_ms = ms;
     c->acc_ms += ms;
+    for (int k = 0; k < c->timed_launches; k++) {
+        float km = 0.f;
+        HIPCHK(c, hipEventElapsedTime(&km, c->kev[2 * k], c->kev[2 * k + 1]));
+        c->acc_kernel_ms += km;
+    }
     c->acc_launches += c->timed_launches;
     c->timed = false;
     return BDPT_OK;
@@ -447,15 +455,13 @@ int bdpt_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int npass
         a.tiles_per_band = tpb;
         grid_rows = owned * tpb;
     }
-    // Pass streams: enough lanes for ~3 rounds of 5 waves per SIMD (a shard of a multi-GPU
-    // frame, or a small image, has fewer pixels than that), else 1.
+    // Pass streams: auto = one pass per lane (S = the launch's pass count).  Eye paths are capped
+    // at 7 segments and most reach the cap, so single-path lanes keep a wave almost perfectly
+    // balanced, while a lane that regenerates through many passes waits for the wave's slowest
+    // sum (+11.7 % at 1080p, and it fills the GPU when a shard has few pixels).
     const long lanes = (long)grid_rows * BDPT_BTH * c->W;
     int S = c->streams_req;
-    if (S == 0) {
-        const long target = 3L * 5 * 4 * c->cus * 64;
-        S = lanes > 0 ? (int)((target + lanes - 1) / lanes) : 1;
-        if (S > 16) S = 16;
-    }
+    if (S == 0) S = BDPT_MAX_STREAMS;
     a.nloc = (int)lanes;
     dim3 grid((c->W + BDPT_BTW - 1) / BDPT_BTW, grid_rows, 1), block(256);
     // keep single launches bounded (~2^28 samples, <= 128 passes for the LDS pass tables)
@@ -466,11 +472,10 @@ int bdpt_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int npass
     if (S > chunk) S = chunk;
     if (S > npass) S = npass;
     if (S < 1) S = 1;
-    a.streams = S;
     c->last_streams = S;
     const bool bvh = c->has_bvh && (c->traversal == BDPT_TRAVERSE_BVH ||
                                     (c->traversal == BDPT_TRAVERSE_AUTO && c->bvh_ns >= kBvhAutoSpheres));
-    const void* kern = bdpt_path_kernel_table[(S > 1) * 18 + (bvh ? 17 : (a.n <= 16 ? a.n : 0))];
+    const int kidx = bvh ? 17 : (a.n <= 16 ? (int)a.n : 0);
     if (bvh) {
         a.bvh_nodes = c->d_bvh_nodes; a.bvh_geom = c->d_bvh_geom; a.bvh_ids = c->d_bvh_ids;
         a.big_geom = c->d_big_geom; a.big_ids = c->d_big_ids; a.mat = c->d_mat;
@@ -493,6 +498,12 @@ int bdpt_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int npass
         }
         a.rbuf = c->d_rbuf;
     }
+    const size_t nchunks = grid_rows > 0 ? (size_t)((npass + chunk - 1) / chunk) : 0;
+    while (c->kev.size() < 2 * nchunks) {
+        hipEvent_t e;
+        HIPCHK(c, hipEventCreate(&e));
+        c->kev.push_back(e);
+    }
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     int launches = 0;
     for (int p0 = 0; grid_rows > 0 && p0 < npass; p0 += chunk, launches++) {
@@ -507,10 +518,15 @@ int bdpt_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int npass
                             + sizeof(unsigned) * (4 * 128 + (size_t)a.npass + ids);
         if (smem > 160 * 1024)
             return fail(c, BDPT_EINVAL, "bdpt_path_passes: scene too large for LDS (%u spheres)", a.n);
+        // S per launch: a short last chunk gets no idle stream slices
+        a.streams = S < a.npass ? S : a.npass;
+        const void* kern = bdpt_path_kernel_table[(a.streams > 1) * 18 + kidx];
         void* kargs[] = {&a};
-        grid.z = S;
+        grid.z = a.streams;
+        HIPCHK(c, hipEventRecord(c->kev[2 * launches], c->stream));
         HIPCHK(c, hipLaunchKernel(kern, grid, block, kargs, smem, c->stream));
-        if (S > 1) {
+        HIPCHK(c, hipEventRecord(c->kev[2 * launches + 1], c->stream));
+        if (a.streams > 1) {
             grid.z = 1;
             HIPCHK(c, hipLaunchKernel((const void*)&bdpt_accum_kernel, grid, block, kargs, 0, c->stream));
         }
@@ -541,7 +557,16 @@ int bdpt_path_timing(bdpt_ctx* c, double* total_ms, long long* launches, int res
     if (int rc = bdpt_synchronize(c)) return rc;
     if (total_ms) *total_ms = c->acc_ms;
     if (launches) *launches = c->acc_launches;
-    if (reset) { c->acc_ms = 0.0; c->acc_launches = 0; }
+    if (reset) { c->acc_ms = 0.0; c->acc_kernel_ms = 0.0; c->acc_launches = 0; }
+    return BDPT_OK;
+}
+
+int bdpt_kernel_timing(bdpt_ctx* c, double* kernel_ms, long long* launches, int reset) {
+    if (!c) return BDPT_EINVAL;
+    if (int rc = bdpt_synchronize(c)) return rc;
+    if (kernel_ms) *kernel_ms = c->acc_kernel_ms;
+    if (launches) *launches = c->acc_launches;
+    if (reset) { c->acc_ms = 0.0; c->acc_kernel_ms = 0.0; c->acc_launches = 0; }
     return BDPT_OK;
 }
 

@@ -74,9 +74,10 @@ int  bdpt_reset_accum(bdpt_ctx *ctx);
  * band_rows a multiple of 8 (the tile height) launches only the shard's own tile rows. */
 int  bdpt_set_shard(bdpt_ctx *ctx, int shard, int nshards, int band_rows);
 /* Pass streams (no reference counterpart; results are bit-identical for every S): S lanes per
- * pixel render passes s, s+S, ... into an HBM radiance buffer and an ordered fold applies the
- * running mean of device.cu:774-787 in pass order.  0 = auto (S > 1 only when the launch has
- * fewer pixels than ~3 rounds of resident waves, e.g. a multi-GPU shard), else 1..128. */
+ * pixel render passes s, s+S, ... into an HBM radiance buffer (12 B per pass and pixel) and an
+ * ordered fold applies the running mean of device.cu:774-787 in pass order.  0 = auto (one pass
+ * per lane: S = passes per launch, <= 128), 1 = the fused kernel that keeps the running mean in
+ * registers (no buffer), else 2..128. */
 int  bdpt_set_streams(bdpt_ctx *ctx, int streams);
 /* S used by the last bdpt_path_passes call. */
 int  bdpt_last_streams(const bdpt_ctx *ctx);
@@ -109,6 +110,9 @@ int  bdpt_last_path_ms(bdpt_ctx *ctx, float *ms);
 /* Accumulated device time and kernel-launch count of all path-pass calls since the last reset
  * (synchronises first).  reset != 0 zeroes the accumulators after reading them. */
 int  bdpt_path_timing(bdpt_ctx *ctx, double *total_ms, long long *launches, int reset);
+/* Same accumulation, but only the path kernels' own durations (one HIP event pair around each
+ * path-kernel launch, excluding the pass-stream fold): what rocprof reports for that kernel. */
+int  bdpt_kernel_timing(bdpt_ctx *ctx, double *kernel_ms, long long *launches, int reset);
 
 /* Read-back.  colors/counter: the float parity artefact (dev_colors / dev_counter);
  * pixels: uchar4 RGBA = pixels_buf (SavePPM, smallpt_cpu.c:241). */

@@ -48,7 +48,16 @@ for k, c in calib.items():
         c["write_bytes_per_reported"] = round(c["write_bytes"] / c["write_reported"], 4)
 fscale = calib.get("gather20", {}).get("line_bytes_per_reported")
 wscale = calib.get("store12", {}).get("write_bytes_per_reported")
-rec = {"scene": "cornell", "width": 1921, "height": 1081, "passes_per_launch": 16.0,
+# the workload of the PMC runs: their own bench.py JSON line
+cfg, roof = {}, {}
+for f in sorted(glob.glob(os.path.join(root, "pmc*.log"))):
+    lines = [l for l in open(f) if l.startswith("{")]
+    if lines:
+        d = json.loads(lines[-1])
+        cfg, roof = d["config"], d.get("roofline") or {}
+        break
+rec = {"scene": cfg.get("scene", "cornell"), "width": cfg.get("width", 1921), "height": cfg.get("height", 1081),
+       "passes_per_launch": float(cfg.get("passes_per_step", 16)), "pass_streams": cfg.get("pass_streams"),
        "fetch_reported_bytes_per_launch": int(fetch), "write_reported_bytes_per_launch": int(write),
        "fetch_scale": fscale, "write_scale": wscale,
        "hbm_bytes_per_launch": int(fetch * (fscale or 1.0) + write * (wscale or 1.0)),

@@ -43,6 +43,7 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--band-rows", type=int, default=8)
     ap.add_argument("--ns", default="1,2,4,8")
+    ap.add_argument("--streams", default="", help="S values to try besides auto, e.g. 1,2,8")
     args = ap.parse_args()
     W, H = 1921, 1081
     cam, sp = g.read_scene(os.path.join(REPO, "assets", "scenes", args.scene + ".scn"))
@@ -52,7 +53,8 @@ def main():
     t1 = None
     for N in [int(x) for x in args.ns.split(",")]:
         sid, vlp = sched.next(args.passes * N * (args.reps + 1))
-        for streams in ([0] if N == 1 else [0, 1]):
+        extra = [int(x) for x in args.streams.split(",") if x] if args.streams else ([] if N == 1 else [1])
+        for streams in [0] + extra:
             worst = 0.0
             for shard in sorted({0, N - 1}):
                 ms, S = run(sp, cam, W, H, sid, vlp, shard, N, args.band_rows, streams, args.reps)

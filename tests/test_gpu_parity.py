@@ -175,17 +175,24 @@ def test_pass_streams_bit_exact(gpu, rnd0, streams):
 
 
 def test_auto_streams_policy(gpu):
-    """Auto: S = 1 for a full 1080p frame, S > 1 for a small frame or an 8-way shard of 1080p."""
+    """Auto: one pass per lane (S = passes in the launch, <= 128); 1 forces the fused kernel."""
     r, _, _ = make("cornell", 1921, 1081, gpu)
-    sid, vlp = schedule(8)
+    sid, vlp = schedule(200)
     r.path_passes(sid[:1], vlp[:1])
     assert r.last_streams == 1
+    r.path_passes(sid[1:9], vlp[1:9])
+    assert r.last_streams == 8
+    r.path_passes(sid[9:200], vlp[9:200])                 # 128 + 63 passes in two launches
+    assert r.last_streams == 128
     r.set_shard(3, 8, 8)
     r.path_passes(sid[:8], vlp[:8])
-    assert r.last_streams == 4
+    assert r.last_streams == 8
+    r.set_streams(1)
+    r.path_passes(sid[:8], vlp[:8])
+    assert r.last_streams == 1
     r.close()
     s, _, _ = make("cornell", 65, 49, gpu)
-    s.path_passes(sid, vlp)
+    s.path_passes(sid[:8], vlp[:8])
     assert s.last_streams == 8
     s.close()
 
