@@ -368,11 +368,13 @@ int bdpt_generate_rand(bdpt_ctx* c, unsigned seed) {
 
 int bdpt_light_pass(bdpt_ctx* c, int current_sample) {
     if (!c) return BDPT_EINVAL;
-    if (c->lights.empty()) return BDPT_OK;                 // the reference launches nothing
     // The reference regenerates the table per light with the same seed (smallpt_cpu.c:321-322):
-    // one generation is identical.
+    // one generation is identical.  With no emitter it launches nothing and the path pass reads
+    // an uninitialised d_Rand; we generate the table anyway (the frame is black either way:
+    // there is no emission, and dev_lp stays zero) so the run is defined.
     int rc = bdpt_generate_rand(c, (unsigned)(current_sample * 5));
     if (rc) return rc;
+    if (c->lights.empty()) return BDPT_OK;
     hipLaunchKernelGGL(bdpt_light_kernel, dim3(BDPT_LIGHT_POINTS / 64), dim3(64), 0, c->stream,
                        (const bdpt_dev_sphere*)c->d_sph, (unsigned)c->spheres.size(),
                        (const float*)c->d_rand, current_sample, c->d_lp);

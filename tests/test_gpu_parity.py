@@ -386,3 +386,54 @@ def test_bvh_1080p_oracle_rows(gpu, rnd0):
         ocol, _, _ = oracle.path_passes(sp, rnd0, cam, W, H, lp, sid, vlp, rows=(y, y + 1))
         assert_same(col[y], ocol[y], f"row {y}")
     r.close()
+
+
+# ---- edge cases: empty scene, no emitter, the N=16/17 kernel boundary, thin frames -----------
+def _render_vs_oracle(gpu, rnd0, cam, sp, W, H, npass, streams=0):
+    g.update_camera(cam, W, H)
+    r = g.Renderer(sp, W, H, cam, device=gpu)
+    r.light_pass(0)
+    r.set_streams(streams)
+    sid, vlp = schedule(npass)
+    r.path_passes(sid, vlp)
+    col, cnt = r.read_radiance()
+    lp = oracle.light_pass(sp, rnd0, 0)
+    assert_same(r.read_lightpaths()["hp"], lp["hp"], "vlp")
+    ocol, ocnt, opix = oracle.path_passes(sp, rnd0, cam, W, H, lp, sid, vlp)
+    assert_same(cnt, ocnt, "counter")
+    assert_same(col, ocol, "colors")
+    assert_same(r.read_pixels(), opix, "pixels")
+    r.close()
+    return col
+
+
+@pytest.mark.parametrize("streams", [0, 1])
+def test_scene_without_emitters(gpu, rnd0, streams):
+    cam, sp = scene("cornell")
+    sp = sp[np.all(sp["e"] == 0, axis=1)].copy()            # drop the light
+    col = _render_vs_oracle(gpu, rnd0, cam, sp, 29, 17, 5, streams)
+    assert (col == 0).all()                                   # no emitter, no light paths: black
+
+
+def test_single_sphere_scene(gpu, rnd0):
+    cam, sp = scene("cornell")
+    _render_vs_oracle(gpu, rnd0, cam, sp[8:9].copy(), 23, 19, 4)   # the light alone
+
+
+@pytest.mark.parametrize("n", [16, 17])
+def test_template_boundary_16_17_spheres(gpu, rnd0, n):
+    """16 spheres: the last compile-time instance (SGPR geometry); 17: the generic LDS kernel."""
+    cam, sp = scene("synthetic64")
+    _render_vs_oracle(gpu, rnd0, cam, np.ascontiguousarray(sp[-n:]), 31, 21, 4)
+
+
+@pytest.mark.parametrize("W,H", [(1921, 1), (1, 301), (37, 9)])
+def test_thin_frames(gpu, rnd0, W, H):
+    cam, sp = scene("cornell_glass")
+    _render_vs_oracle(gpu, rnd0, cam, sp, W, H, 3)
+
+
+def test_empty_scene(gpu, rnd0):
+    cam, sp = scene("cornell")
+    col = _render_vs_oracle(gpu, rnd0, cam, sp[:0].copy(), 13, 7, 3)
+    assert (col == 0).all()
