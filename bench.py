@@ -95,6 +95,8 @@ def main():
     ap.add_argument("--streams", type=int, default=0, help="pass streams per pixel (0 = auto)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--rehearse", action="store_true",
+                    help="multi-rank dry run on fewer GPUs: gloo, ranks share devices (not a measurement)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -106,11 +108,16 @@ def main():
     import gpu_bidirectional_raytracer_amd as g
     from gpu_bidirectional_raytracer_amd import sharding as shd
 
+    if args.rehearse:
+        local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     W, H = args.width + 1, args.height + 1                   # smallpt_cpu.c:409-410
     cam, sp = g.read_scene(os.path.join(REPO, "assets", "scenes", args.scene + ".scn"))
@@ -155,7 +162,7 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
     if dist is not None:
-        tt = torch.tensor([dt], device=f"cuda:{local}", dtype=torch.float64)
+        tt = torch.tensor([dt], device="cpu" if args.rehearse else f"cuda:{local}", dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
 
@@ -224,6 +231,8 @@ def main():
         }
         if cpu:
             line["speedup_vs_cpu"] = round(value / cpu["value"], 1)
+        if args.rehearse:
+            line["rehearsal"] = "ranks share GPUs over gloo: exercises the multi-rank flow, not a measurement"
         print(json.dumps(line), flush=True)
     r.close()
     if dist is not None:

@@ -50,8 +50,16 @@ def device_tensors(renderer, device):
 
 
 def reduce_frame(t_col, t_cnt, dst: int = 0) -> None:
-    """Sum-reduce the zero-padded per-rank frames to `dst` (exact: disjoint pixel support)."""
+    """Sum-reduce the zero-padded per-rank frames to `dst` (exact: disjoint pixel support).
+    RCCL ("nccl") reduces the device buffers in place; a gloo group (CPU tests, multi-rank
+    rehearsals on one GPU) stages them through host memory."""
     import torch.distributed as dist
 
-    dist.reduce(t_col, dst=dst, op=dist.ReduceOp.SUM)
-    dist.reduce(t_cnt, dst=dst, op=dist.ReduceOp.SUM)
+    for t in (t_col, t_cnt):
+        if t.is_cuda and dist.get_backend() == "gloo":
+            h = t.cpu()
+            dist.reduce(h, dst=dst, op=dist.ReduceOp.SUM)
+            if dist.get_rank() == dst:
+                t.copy_(h)
+        else:
+            dist.reduce(t, dst=dst, op=dist.ReduceOp.SUM)
