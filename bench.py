@@ -209,6 +209,13 @@ def main():
                     "flop_per_sample": round(flop_per_sample(w), 1),
                     "note": "bound: fp32 VALU (no contraction, correctly rounded div/sqrt); "
                             "FLOP model in DESIGN.md"}
+            pv = os.path.join(REPO, "profiles", "pmc_valu.json")
+            if os.path.exists(pv) and world == 1:
+                rec = json.load(open(pv))
+                if rec.get("scene") == args.scene and rec.get("passes_per_launch") == passes_per_launch \
+                        and rec.get("pass_streams") == r.last_streams and rec.get("width") == W:
+                    valu["busy_pmc"] = rec["valu_busy"]
+                    valu["lane_utilisation_pmc"] = rec["valu_lane_utilisation"]
             if r.last_traversal == "bvh":
                 valu["note"] = ("reference-equivalent FLOPs: the reference tests every sphere; the BVH "
                                 "skips most tests, so this is work avoided, not VALU throughput")

@@ -23,3 +23,21 @@ print(f"VALU busy (instr*2/(4*256*cyc)) {g('SQ_INSTS_VALU') * 2 / (4 * 256 * cyc
 print(f"SALU / VALU instr           {g('SQ_INSTS_SALU') / g('SQ_INSTS_VALU'):.3f}")
 print(f"L2 hit rate                 {g('TCC_HIT_sum') / (g('TCC_HIT_sum') + g('TCC_MISS_sum')):.3f}")
 print(f"FETCH (MB) / WRITE (MB)     {g('FETCH_SIZE') / 1024:.1f} / {g('WRITE_SIZE') / 1024:.1f}")
+# optional: python scripts/pmc_summary.py <root> <kernel> <pattern> <out.json> -- the derived
+# figures plus the bench configuration of the PMC runs, read by bench.py into its `valu` object
+if len(sys.argv) > 4:
+    import json
+    cfg = {}
+    for f in sorted(glob.glob(os.path.join(root, pat + ".log"))):
+        lines = [l for l in open(f) if l.startswith("{")]
+        if lines:
+            cfg = json.loads(lines[-1])["config"]
+            break
+    rec = {"valu_busy": round(g('SQ_INSTS_VALU') * 2 / (4 * 256 * cyc), 4),
+           "valu_lane_utilisation": round(g('SQ_THREAD_CYCLES_VALU') / (64 * g('SQ_ACTIVE_INST_VALU')), 4),
+           "l2_hit_rate": round(g('TCC_HIT_sum') / (g('TCC_HIT_sum') + g('TCC_MISS_sum')), 4),
+           "scene": cfg.get("scene"), "width": cfg.get("width"), "height": cfg.get("height"),
+           "passes_per_launch": cfg.get("passes_per_step"), "pass_streams": cfg.get("pass_streams"),
+           "source": "rocprofv3 --pmc SQ_INSTS_VALU / SQ_THREAD_CYCLES_VALU / SQ_ACTIVE_INST_VALU / "
+                     "GRBM_GUI_ACTIVE / TCC_HIT_sum / TCC_MISS_sum (separate passes), scripts/pmc_summary.py"}
+    json.dump(rec, open(sys.argv[4], "w"), indent=1)
