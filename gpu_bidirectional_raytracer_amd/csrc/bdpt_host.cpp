@@ -514,8 +514,13 @@ int bdpt_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int npass
         a.npass = npass - p0 < chunk ? npass - p0 : chunk;
         // scene tables (4 per sphere, or the BVH: 2 per node + 1 per sphere) + per-pass VLPs +
         // camera + 4 wave shadow queues + results + sids (+ BVH sphere ids)
-        const size_t tab = bvh ? 2 * (size_t)a.bvh_nn + a.bvh_ns + a.big_n : 4 * (size_t)a.n;
-        const size_t ids = bvh ? (size_t)a.bvh_ns + a.big_n : 0;
+#ifdef BDPT_BVH_LDS
+        const size_t tree = 2 * (size_t)a.bvh_nn + a.bvh_ns, tree_ids = a.bvh_ns;
+#else
+        const size_t tree = 0, tree_ids = 0;                 // tree read through L1/L2
+#endif
+        const size_t tab = bvh ? tree + a.big_n : 4 * (size_t)a.n;
+        const size_t ids = bvh ? tree_ids + a.big_n : 0;
         const size_t smem = sizeof(float4) * (tab + 3 * (size_t)a.npass + 5 + 4 * 128 * 2)
                             + sizeof(unsigned) * (4 * 128 + (size_t)a.npass + ids);
         if (smem > 160 * 1024)

@@ -306,33 +306,44 @@ __device__ __forceinline__ bool bvh_box(float4 lo, float4 hi, const bvh_ray& r, 
 #ifndef BDPT_WAVES_PER_SIMD
 #define BDPT_WAVES_PER_SIMD 5
 #endif
-// BVH scenes hold ~30 KB of tree in LDS per workgroup (4 per CU): 4 waves/SIMD, 128 VGPRs.
+// BVH scenes: 4 waves/SIMD (128 VGPRs; the traversal state does not fit 96).
 template <int N, bool STREAMS>
 __global__ __launch_bounds__(256, N < 0 ? 4 : BDPT_WAVES_PER_SIMD) void bdpt_path_kernel_t(bdpt_path_args a) {
     extern __shared__ float4 smem[];
     constexpr bool kBVH = N < 0;      // large scene: walls brute force + BVH (bdpt_bvh.cpp)
     const int n = N > 0 ? N : (int)a.n;
     constexpr int kUnroll = N > 0 ? N : 1;
-    const int ntab = kBVH ? 2 * a.bvh_nn + a.bvh_ns + a.big_n : 4 * n;
+#ifdef BDPT_BVH_LDS
+    constexpr bool kTreeLds = true;   // tree copied to LDS per workgroup (3 per CU)
+#else
+    constexpr bool kTreeLds = false;  // tree read through L1/L2: 4 workgroups per CU (+10 %)
+#endif
+    const int ntree = kTreeLds ? 2 * a.bvh_nn + a.bvh_ns : 0;
+    const int ntab = kBVH ? ntree + a.big_n : 4 * n;
     float4* C = smem;                 // {cx, cy, cz, bits(refl | emissive<<8)}
     float4* E = smem + n;             // {ex, ey, ez, rad}
     float4* P = smem + 2 * n;         // {px, py, pz, 0}  (hit normal)
     float4* G = smem + 3 * n;         // {px, py, pz, rad^2}  (N == 0 traversal)
     float4* ND = smem;                // BVH: nodes (2 float4 each)
     float4* SG = ND + 2 * a.bvh_nn;   // BVH: sphere geometry in leaf order
-    float4* BG = SG + a.bvh_ns;       // BVH: brute-force (wall) geometry
+    float4* BG = smem + ntree;        // BVH: brute-force (wall) geometry
     float4* V = smem + ntab;          // per pass: VLP {hx,hy,hz,rx}{ry,rz,nx,ny}{nz,-,-,-}
     float4* K = V + 3 * a.npass;      // camera constants (5 float4)
     float4* Q = K + 5;                // shadow queues: 4 waves x kQueue x 2 float4
     unsigned* R = (unsigned*)(Q + 4 * kQueue * 2);    // shadow results: 4 x kQueue
     unsigned* SID = R + 4 * kQueue;   // per pass sid
     int* SI = (int*)(SID + a.npass);  // BVH: sphere ids (| emissive flag), leaf order
-    int* BI = SI + a.bvh_ns;          // BVH: wall ids
+    int* BI = SI + (kTreeLds ? a.bvh_ns : 0);   // BVH: wall ids
+    const float4* __restrict__ NDt = kTreeLds ? (const float4*)ND : a.bvh_nodes;
+    const float4* __restrict__ SGt = kTreeLds ? (const float4*)SG : a.bvh_geom;
+    const int* __restrict__ SIt = kTreeLds ? (const int*)SI : a.bvh_ids;
     if constexpr (kBVH) {
-        for (int q = threadIdx.x; q < 2 * a.bvh_nn; q += 256) ND[q] = a.bvh_nodes[q];
-        for (int q = threadIdx.x; q < a.bvh_ns; q += 256) {
-            SG[q] = a.bvh_geom[q];
-            SI[q] = a.bvh_ids[q];
+        if constexpr (kTreeLds) {
+            for (int q = threadIdx.x; q < 2 * a.bvh_nn; q += 256) ND[q] = a.bvh_nodes[q];
+            for (int q = threadIdx.x; q < a.bvh_ns; q += 256) {
+                SG[q] = a.bvh_geom[q];
+                SI[q] = a.bvh_ids[q];
+            }
         }
         for (int q = threadIdx.x; q < a.big_n; q += 256) {
             BG[q] = a.big_geom[q];
@@ -454,7 +465,7 @@ __global__ __launch_bounds__(256, N < 0 ? 4 : BDPT_WAVES_PER_SIMD) void bdpt_pat
                 while (true) {
                     int info = -1;
                     while (node < a.bvh_nn) {
-                        const float4 lo = ND[2 * node], hi = ND[2 * node + 1];
+                        const float4 lo = NDt[2 * node], hi = NDt[2 * node + 1];
                         const int inf = __float_as_int(hi.w);
                         const bool in = bvh_box(lo, hi, br, t);
                         node = (in && inf < 0) ? node + 1 : __float_as_int(lo.w);
@@ -463,8 +474,8 @@ __global__ __launch_bounds__(256, N < 0 ? 4 : BDPT_WAVES_PER_SIMD) void bdpt_pat
                     if (info < 0) break;
                     const int first = info & 0xffffff, end = first + (info >> 24);
                     for (int k = first; k < end; k++) {
-                        const float d = sphere_isect_inf(SG[k], ro, rd);
-                        const int s = SI[k] & kBvhIdMask;
+                        const float d = sphere_isect_inf(SGt[k], ro, rd);
+                        const int s = SIt[k] & kBvhIdMask;
                         if (d < t || (d == t && s > id)) { t = d; id = s; }
                     }
                 }
@@ -616,14 +627,14 @@ __global__ __launch_bounds__(256, N < 0 ? 4 : BDPT_WAVES_PER_SIMD) void bdpt_pat
                             const bvh_ray br = bvh_setup(a, o, d);
                             int node = occ ? a.bvh_nn : 0;
                             while (node < a.bvh_nn) {
-                                const float4 lo = ND[2 * node], hi = ND[2 * node + 1];
+                                const float4 lo = NDt[2 * node], hi = NDt[2 * node + 1];
                                 const int info = __float_as_int(hi.w);
                                 if (!bvh_box(lo, hi, br, r0.w)) { node = __float_as_int(lo.w); continue; }
                                 if (info < 0) { node++; continue; }
                                 const int first = info & 0xffffff, end = first + (info >> 24);
                                 for (int k = first; k < end; k++) {
-                                    const float dd = sphere_isect_inf(SG[k], o, d);
-                                    if (dd < r0.w && !(vac && (SI[k] & kBvhEmissive))) { occ = 1; break; }
+                                    const float dd = sphere_isect_inf(SGt[k], o, d);
+                                    if (dd < r0.w && !(vac && (SIt[k] & kBvhEmissive))) { occ = 1; break; }
                                 }
                                 node = occ ? a.bvh_nn : __float_as_int(lo.w);
                             }
