@@ -306,9 +306,13 @@ __device__ __forceinline__ bool bvh_box(float4 lo, float4 hi, const bvh_ray& r, 
 #ifndef BDPT_WAVES_PER_SIMD
 #define BDPT_WAVES_PER_SIMD 5
 #endif
-// BVH scenes: 4 waves/SIMD (128 VGPRs; the traversal state does not fit 96).
+// BVH scenes: 5 waves/SIMD too, although the traversal state spills 10 VGPRs at 96 (measured:
+// 4 waves +0 spills is 10-12 % slower, 6 waves spills 27).
+#ifndef BDPT_BVH_WAVES
+#define BDPT_BVH_WAVES 5
+#endif
 template <int N, bool STREAMS>
-__global__ __launch_bounds__(256, N < 0 ? 4 : BDPT_WAVES_PER_SIMD) void bdpt_path_kernel_t(bdpt_path_args a) {
+__global__ __launch_bounds__(256, N < 0 ? BDPT_BVH_WAVES : BDPT_WAVES_PER_SIMD) void bdpt_path_kernel_t(bdpt_path_args a) {
     extern __shared__ float4 smem[];
     constexpr bool kBVH = N < 0;      // large scene: walls brute force + BVH (bdpt_bvh.cpp)
     const int n = N > 0 ? N : (int)a.n;
