@@ -40,13 +40,23 @@ extern "C" void bdpt_gamma_thresholds(float thr[256]);
 struct bdpt_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    bool timed = false;          // an event pair of a path-pass call is outstanding
-    int timed_launches = 0;      // kernel launches inside that pair
+    // Path-pass calls go through a ring of kRing slots, each with its own pinned staging and
+    // device copy of the pass tables (sid, vlp) and its own events, so a call never waits for
+    // the GPU except on the call issued kRing calls earlier (the reference's interactive loop
+    // issues one pass per call).  Timing is folded lazily, in call order.
+    static constexpr int kRing = 4;
+    struct call_slot {
+        hipEvent_t ev0 = nullptr, ev1 = nullptr;   // the whole call
+        std::vector<hipEvent_t> kev;               // per path-kernel launch {before, after}
+        int launches = 0;
+        bool pending = false;                      // issued, not folded yet
+    } ring[kRing];
+    long long issued = 0, folded = 0;   // calls issued / folded into the accumulators
+    unsigned* h_pass = nullptr;         // pinned staging, kRing x (2 x pass_cap)
+    unsigned* d_pass = nullptr;         // device tables, kRing x (2 x pass_cap): sid..., vlp...
     double acc_ms = 0.0;         // accumulated device time of finished path-pass calls
     long long acc_launches = 0;
     float last_ms = 0.f;
-    std::vector<hipEvent_t> kev;   // per path-kernel launch: {before, after} (pool, reused)
     double acc_kernel_ms = 0.0;    // path kernels alone (no fold kernel)
     int W = 0, H = 0;
     std::vector<bdpt_sphere> spheres;
@@ -80,8 +90,6 @@ struct bdpt_ctx {
     unsigned* d_counter = nullptr;
     uchar4* d_pixels = nullptr;
     float* d_thr = nullptr;
-    unsigned* d_sid = nullptr;
-    int* d_vlp = nullptr;
     int pass_cap = 0;
     uint32_t h_params[4 * BDPT_MT_RNG_COUNT];
     char err[512] = {0};
@@ -106,6 +114,8 @@ static int fail(bdpt_ctx* c, int code, const char* fmt, ...) {
 
 static int upload_scene(bdpt_ctx* c) {
     const unsigned n = (unsigned)c->spheres.size();
+    // queued path passes may still read the scene buffers freed / rewritten below
+    HIPCHK(c, hipStreamSynchronize(c->stream));
     std::vector<bdpt_dev_sphere> ds(n);
     std::vector<float4> geom(n), lrec;
     c->lights.clear();
@@ -196,33 +206,41 @@ static int upload_scene(bdpt_ctx* c) {
 
 static void release(bdpt_ctx* c) {
     void* bufs[] = {c->d_params, c->d_rand, c->d_lp, c->d_sph, c->d_lights, c->d_geom, c->d_lightrec, c->d_colors,
-                    c->d_counter, c->d_pixels, c->d_thr, c->d_sid, c->d_vlp, c->d_rbuf, c->d_bvh_nodes,
+                    c->d_counter, c->d_pixels, c->d_thr, c->d_pass, c->d_rbuf, c->d_bvh_nodes,
                     c->d_bvh_geom, c->d_big_geom, c->d_mat, c->d_bvh_ids, c->d_big_ids};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
-    for (hipEvent_t e : c->kev) (void)hipEventDestroy(e);
-    if (c->ev0) (void)hipEventDestroy(c->ev0);
-    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    for (auto& s : c->ring) {
+        for (hipEvent_t e : s.kev) (void)hipEventDestroy(e);
+        if (s.ev0) (void)hipEventDestroy(s.ev0);
+        if (s.ev1) (void)hipEventDestroy(s.ev1);
+    }
+    if (c->h_pass) (void)hipHostFree(c->h_pass);
     if (c->stream) (void)hipStreamDestroy(c->stream);
 }
 
-// Fold the outstanding event pair (if any) into the accumulators.  Caller has synchronised.
-static int fold_timing(bdpt_ctx* c) {
-    if (!c->timed) return BDPT_OK;
-    float ms = 0.f;
-    HIPCHK(c, hipEventSynchronize(c->ev1));
-    HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
-    c->last_ms = ms;
-    c->acc_ms += ms;
-    for (int k = 0; k < c->timed_launches; k++) {
-        float km = 0.f;
-        HIPCHK(c, hipEventElapsedTime(&km, c->kev[2 * k], c->kev[2 * k + 1]));
-        c->acc_kernel_ms += km;
+// Fold the calls issued before call number `upto` into the accumulators, oldest first (waits
+// for each of them to finish).
+static int fold_timing(bdpt_ctx* c, long long upto) {
+    for (; c->folded < upto && c->folded < c->issued; c->folded++) {
+        bdpt_ctx::call_slot& s = c->ring[c->folded % bdpt_ctx::kRing];
+        if (!s.pending) continue;
+        float ms = 0.f;
+        HIPCHK(c, hipEventSynchronize(s.ev1));
+        HIPCHK(c, hipEventElapsedTime(&ms, s.ev0, s.ev1));
+        c->last_ms = ms;
+        c->acc_ms += ms;
+        for (int k = 0; k < s.launches; k++) {
+            float km = 0.f;
+            HIPCHK(c, hipEventElapsedTime(&km, s.kev[2 * k], s.kev[2 * k + 1]));
+            c->acc_kernel_ms += km;
+        }
+        c->acc_launches += s.launches;
+        s.pending = false;
     }
-    c->acc_launches += c->timed_launches;
-    c->timed = false;
     return BDPT_OK;
 }
+static int fold_timing(bdpt_ctx* c) { return fold_timing(c, c->issued); }
 
 extern "C" {
 
@@ -263,8 +281,10 @@ int bdpt_create(bdpt_ctx** out, const bdpt_sphere* spheres, unsigned n, int W, i
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
             c->cus = cus;
     }
-    CK(hipEventCreate(&c->ev0));
-    CK(hipEventCreate(&c->ev1));
+    for (auto& s : c->ring) {
+        CK(hipEventCreate(&s.ev0));
+        CK(hipEventCreate(&s.ev1));
+    }
     const size_t np = (size_t)W * H;
     CK(hipMalloc(&c->d_params, sizeof(c->h_params)));
     CK(hipMalloc(&c->d_rand, sizeof(float) * BDPT_RAND_N));
@@ -396,20 +416,29 @@ int bdpt_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int npass
     if (!c->rand_ready) return fail(c, BDPT_ESTATE, "bdpt_path_passes: no random table (run the light pass first)");
     if (!c->cam_set) return fail(c, BDPT_ESTATE, "bdpt_path_passes: camera not set");
     HIPCHK(c, hipSetDevice(c->device));
-    // the previous launch may still read d_sid/d_vlp: drain the stream before overwriting them
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    if (int rc = fold_timing(c)) return rc;
-    if (npass > c->pass_cap) {
-        if (c->d_sid) HIPCHK(c, hipFree(c->d_sid));
-        if (c->d_vlp) HIPCHK(c, hipFree(c->d_vlp));
-        c->d_sid = nullptr; c->d_vlp = nullptr;
-        int cap = npass < 1024 ? 1024 : npass;
-        HIPCHK(c, hipMalloc(&c->d_sid, sizeof(unsigned) * cap));
-        HIPCHK(c, hipMalloc(&c->d_vlp, sizeof(int) * cap));
+    // this call's ring slot was last used kRing calls ago: wait for (only) that call
+    const int slot = (int)(c->issued % bdpt_ctx::kRing);
+    if (int rc = fold_timing(c, c->issued - bdpt_ctx::kRing + 1)) return rc;
+    if (npass > c->pass_cap) {                              // grow every slot (drain first)
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (int rc = fold_timing(c)) return rc;
+        if (c->d_pass) HIPCHK(c, hipFree(c->d_pass));
+        if (c->h_pass) HIPCHK(c, hipHostFree(c->h_pass));
+        c->d_pass = nullptr; c->h_pass = nullptr;
+        const int cap = npass < 1024 ? 1024 : npass;
+        const size_t words = (size_t)bdpt_ctx::kRing * 2 * cap;
+        HIPCHK(c, hipMalloc(&c->d_pass, sizeof(unsigned) * words));
+        HIPCHK(c, hipHostMalloc(&c->h_pass, sizeof(unsigned) * words, hipHostMallocDefault));
         c->pass_cap = cap;
     }
-    HIPCHK(c, hipMemcpy(c->d_sid, sid, sizeof(unsigned) * npass, hipMemcpyHostToDevice));
-    HIPCHK(c, hipMemcpy(c->d_vlp, vlp, sizeof(int) * npass, hipMemcpyHostToDevice));
+    unsigned* hs = c->h_pass + (size_t)slot * 2 * c->pass_cap;
+    unsigned* ds = c->d_pass + (size_t)slot * 2 * c->pass_cap;
+    memcpy(hs, sid, sizeof(unsigned) * npass);
+    memcpy(hs + npass, vlp, sizeof(int) * npass);
+    HIPCHK(c, hipMemcpyAsync(ds, hs, sizeof(unsigned) * 2 * npass, hipMemcpyHostToDevice, c->stream));
+    const unsigned* d_sid = ds;
+    const int* d_vlp = (const int*)(ds + npass);
+    bdpt_ctx::call_slot& cs = c->ring[slot];
 
     bdpt_path_args a;
     memset(&a, 0, sizeof(a));
@@ -491,6 +520,7 @@ int bdpt_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int npass
         const int cmax = npass < chunk ? npass : chunk;
         const size_t need = (size_t)cmax * (size_t)lanes;
         if (need > c->rbuf_cap) {
+            HIPCHK(c, hipStreamSynchronize(c->stream));     // queued passes may use it
             if (c->d_rbuf) HIPCHK(c, hipFree(c->d_rbuf));
             c->d_rbuf = nullptr;
             c->rbuf_cap = 0;
@@ -501,16 +531,16 @@ int bdpt_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int npass
         a.rbuf = c->d_rbuf;
     }
     const size_t nchunks = grid_rows > 0 ? (size_t)((npass + chunk - 1) / chunk) : 0;
-    while (c->kev.size() < 2 * nchunks) {
+    while (cs.kev.size() < 2 * nchunks) {
         hipEvent_t e;
         HIPCHK(c, hipEventCreate(&e));
-        c->kev.push_back(e);
+        cs.kev.push_back(e);
     }
-    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+    HIPCHK(c, hipEventRecord(cs.ev0, c->stream));
     int launches = 0;
     for (int p0 = 0; grid_rows > 0 && p0 < npass; p0 += chunk, launches++) {
-        a.sid = c->d_sid + p0;
-        a.vlp = c->d_vlp + p0;
+        a.sid = d_sid + p0;
+        a.vlp = d_vlp + p0;
         a.npass = npass - p0 < chunk ? npass - p0 : chunk;
         // scene tables (4 per sphere, or the BVH: 2 per node + 1 per sphere) + per-pass VLPs +
         // camera + 4 wave shadow queues + results + sids (+ BVH sphere ids)
@@ -530,17 +560,18 @@ int bdpt_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int npass
         const void* kern = bdpt_path_kernel_table[(a.streams > 1) * 18 + kidx];
         void* kargs[] = {&a};
         grid.z = a.streams;
-        HIPCHK(c, hipEventRecord(c->kev[2 * launches], c->stream));
+        HIPCHK(c, hipEventRecord(cs.kev[2 * launches], c->stream));
         HIPCHK(c, hipLaunchKernel(kern, grid, block, kargs, smem, c->stream));
-        HIPCHK(c, hipEventRecord(c->kev[2 * launches + 1], c->stream));
+        HIPCHK(c, hipEventRecord(cs.kev[2 * launches + 1], c->stream));
         if (a.streams > 1) {
             grid.z = 1;
             HIPCHK(c, hipLaunchKernel((const void*)&bdpt_accum_kernel, grid, block, kargs, 0, c->stream));
         }
     }
-    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
-    c->timed = true;
-    c->timed_launches = launches;
+    HIPCHK(c, hipEventRecord(cs.ev1, c->stream));
+    cs.launches = launches;
+    cs.pending = true;
+    c->issued++;
     return BDPT_OK;
 }
 

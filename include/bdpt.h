@@ -102,7 +102,8 @@ int  bdpt_generate_rand(bdpt_ctx *ctx, unsigned seed);
 
 /* `npass` x UpdateRendering (smallpt_cpu.c:265-297) fused into one launch: pass p uses
  * sid[p] (= rand()%RAND_N, :270) and vlp_index[p] (the :292-293 state machine).
- * Asynchronous on the context's stream; bdpt_synchronize() waits. */
+ * Asynchronous on the context's stream (a call only waits for the call issued 4 calls earlier,
+ * whose pass-table slot it reuses); bdpt_synchronize() waits for all. */
 int  bdpt_path_passes(bdpt_ctx *ctx, const unsigned *sid, const int *vlp_index, int npass);
 int  bdpt_synchronize(bdpt_ctx *ctx);
 /* Device time (ms, HIP events on the context's stream) of the last bdpt_path_passes call. */
@@ -120,7 +121,8 @@ int  bdpt_read_radiance(bdpt_ctx *ctx, bdpt_vec *colors, unsigned *counter);
 int  bdpt_read_pixels(bdpt_ctx *ctx, unsigned char *rgba);
 int  bdpt_read_rand(bdpt_ctx *ctx, float *rand_table);          /* d_Rand, BDPT_RAND_N */
 int  bdpt_read_lightpaths(bdpt_ctx *ctx, bdpt_lightpath *lp);   /* dev_lp, 4096        */
-/* Device pointers for zero-copy collectives (RCCL reduce of the radiance frame). */
+/* Device pointers for zero-copy collectives (RCCL reduce of the radiance frame).  Path passes
+ * run asynchronously on the context's own stream: bdpt_synchronize() before using them. */
 int  bdpt_device_buffers(bdpt_ctx *ctx, void **colors, void **counter, void **pixels);
 /* Recompute pixels (toInt gamma) from colors on the device, e.g. after a cross-GPU reduce. */
 int  bdpt_update_pixels(bdpt_ctx *ctx);
