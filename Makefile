@@ -23,7 +23,7 @@ all: $(LIB) $(HOST) $(ORACLE)
 $(BUILD):
 	mkdir -p $(BUILD)
 
-$(BUILD)/bdpt_kernels.o: $(CSRC)/bdpt_kernels.hip $(CSRC)/bdpt_device.h $(CSRC)/bdpt_math.h | $(BUILD)
+$(BUILD)/bdpt_kernels.o: $(CSRC)/bdpt_kernels.hip $(CSRC)/bdpt_device.h $(CSRC)/bdpt_math.h $(CSRC)/bdpt_sincos_table.h | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(BUILD)/bdpt_host.o: $(CSRC)/bdpt_host.cpp $(CSRC)/bdpt_device.h $(CSRC)/bdpt_bvh.h include/bdpt.h | $(BUILD)

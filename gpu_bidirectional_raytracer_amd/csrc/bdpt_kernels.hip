@@ -39,13 +39,21 @@ constexpr float kEps = 0.01f;                              // geom.h:6 EPSILON
 constexpr float kPi = 3.14159265358979323846f;             // geom.h:7 FLOAT_PI
 constexpr unsigned kRandN = BDPT_DEV_RAND_N;
 
-// sinf/cosf with correctly-rounded semantics: fp64 sincos rounded once to fp32 (bdpt_math.h).
-__device__ __forceinline__ void sincos_cr(float x, float* s, float* c) {
+// the table of bdpt_sincos_tab in device memory (copied to LDS by the path kernel)
+__device__ const double bdpt_sincos_table_dev[256][2] = BDPT_SINCOS_TABLE_INIT;
+
+// sinf/cosf with correctly-rounded semantics: fp64 sincos rounded once to fp32 (bdpt_math.h),
+// table-driven when the caller has the {sin, cos}(k pi/128) table in LDS.
+#ifndef BDPT_SINCOS_TABLE
+#define BDPT_SINCOS_TABLE 1
+#endif
+__device__ __forceinline__ void sincos_cr(float x, float* s, float* c, const double* tab = nullptr) {
 #ifdef BDPT_ABL_SINCOS
     *s = __sinf(x); *c = __cosf(x); return;
 #endif
     double sd, cd;
-    bdpt_sincos_dp((double)x, &sd, &cd);
+    if (BDPT_SINCOS_TABLE && tab) bdpt_sincos_tab((double)x, tab, &sd, &cd);
+    else bdpt_sincos_dp((double)x, &sd, &cd);
     *s = (float)sd;
     *c = (float)cd;
 }
@@ -78,18 +86,18 @@ __device__ __forceinline__ float sphere_isect_inf(float4 g, f3 o, f3 d) {
 }
 
 // UniformSampleSphereDevice device.cu:157-165
-__device__ __forceinline__ f3 uniform_sphere(float u1, float u2) {
+__device__ __forceinline__ f3 uniform_sphere(float u1, float u2, const double* tab = nullptr) {
     const float zz = 1.f - 2.f * u1;
     const float q = 1.f - zz * zz;
     const float r = bdpt_sqrt_rn_core(0.f > q ? 0.f : q);   // q is 0 or >= 2^-24: core is exact
     const float phi = 2.f * kPi * u2;
     float s, c;
-    sincos_cr(phi, &s, &c);
+    sincos_cr(phi, &s, &c, tab);
     return mk(r * c, r * s, zz);
 }
 
 // Cosine-weighted direction about w (device.cu:676-699; also :190-212 and :357-380).
-__device__ __forceinline__ f3 cosine_dir(f3 w, float u_phi, float u_r2) {
+__device__ __forceinline__ f3 cosine_dir(f3 w, float u_phi, float u_r2, const double* tab = nullptr) {
     const float r1 = 2.f * kPi * u_phi;
     const float r2 = u_r2;
     const float r2s = bdpt_sqrt_rn_core(r2);                 // r2 = d_Rand value >= 2^-32
@@ -98,7 +106,7 @@ __device__ __forceinline__ f3 cosine_dir(f3 w, float u_phi, float u_r2) {
     f3 u = smul(1.f / bdpt_sqrt_rn_core(dot(uc, uc)), uc);
     f3 v = cross(w, u);
     float s, c;
-    sincos_cr(r1, &s, &c);
+    sincos_cr(r1, &s, &c, tab);
     u = smul(c * r2s, u);
     v = smul(s * r2s, v);
     f3 nd = add(u, v);
@@ -377,6 +385,13 @@ __global__ __launch_bounds__(256, N < 0 ? BDPT_BVH_WAVES : BDPT_WAVES_PER_SIMD) 
         K[3] = make_float4(a.orig[0], a.orig[1], a.orig[2], 0.f);
         K[4] = make_float4(a.inv_w, a.inv_h, 0.f, 0.f);
     }
+    // {sin, cos}(k pi/128) for the table-driven sincos (bdpt_math.h), 4 KB, one entry per thread
+    __shared__ double2 sct[256];
+    {
+        const double* t = &bdpt_sincos_table_dev[0][0];
+        sct[threadIdx.x] = make_double2(t[2 * threadIdx.x], t[2 * threadIdx.x + 1]);
+    }
+    const double* SCT = (const double*)sct;
     __syncthreads();
 
     auto geom = [&](int s) -> float4 {
@@ -510,7 +525,7 @@ __global__ __launch_bounds__(256, N < 0 ? BDPT_BVH_WAVES : BDPT_WAVES_PER_SIMD) 
                     thr = mul(thr, mk(cm.x, cm.y, cm.z));
                     diff = true;                  // shadow rays: below, compacted over the wave
                     ro = hit;
-                    rd = cosine_dir(nl, q0, q1);
+                    rd = cosine_dir(nl, q0, q1, SCT);
                 } else if ((mat & 255) == BDPT_DEV_SPEC) {               // :704-714
                     specular = true;
                     const f3 nd = sub(rd, smul(2.f * dot(normal, rd), normal));
@@ -557,7 +572,7 @@ __global__ __launch_bounds__(256, N < 0 ? BDPT_BVH_WAVES : BDPT_WAVES_PER_SIMD) 
         // NEE towards every emitter (same d_Rand[j+3], d_Rand[j+4] for all) + 1 VLP, blended 1/2.
         if (__builtin_amdgcn_ballot_w64(diff) != 0) {
             f3 res = mk(0.f, 0.f, 0.f), usp = res, vsd = res, vcon = res;
-            if (diff) usp = uniform_sphere(q3, q4);
+            if (diff) usp = uniform_sphere(q3, q4, SCT);
             const int nsteps = a.n_lights > 0 ? (int)a.n_lights : 1;
             for (int li = 0; li < nsteps; li++) {                         // uniform
                 bool has_nee = false, has_vlp = false;

@@ -17,7 +17,8 @@ int main(int argc, char **argv)
     uint32_t b0, b1;
     memcpy(&b0, &lo, 4);
     memcpy(&b1, &hi, 4);
-    long n = 0, bad = 0;
+    static const double tab[256][2] = BDPT_SINCOS_TABLE_INIT;
+    long n = 0, bad = 0, bad_tab = 0;
     for (uint64_t b = b0; b <= b1; b += stride) {
         uint32_t bb = (uint32_t)b;
         float f;
@@ -26,12 +27,18 @@ int main(int argc, char **argv)
         const float x = 2.f * 3.14159265358979323846f * u;
         double s, c;
         bdpt_sincos_dp((double)x, &s, &c);
-        if ((float)s != (float)sin((double)x) || (float)c != (float)cos((double)x)) {
+        const float gs = (float)sin((double)x), gc = (float)cos((double)x);
+        if ((float)s != gs || (float)c != gc) {
             if (bad < 5) printf("mismatch u=%a x=%a\n", u, x);
             bad++;
         }
+        bdpt_sincos_tab((double)x, &tab[0][0], &s, &c);
+        if ((float)s != gs || (float)c != gc) {
+            if (bad_tab < 5) printf("table mismatch u=%a x=%a\n", u, x);
+            bad_tab++;
+        }
         n++;
     }
-    printf("checked %ld inputs, %ld mismatches\n", n, bad);
-    return bad != 0;
+    printf("checked %ld inputs, %ld mismatches, %ld table-version mismatches\n", n, bad, bad_tab);
+    return bad != 0 || bad_tab != 0;
 }
