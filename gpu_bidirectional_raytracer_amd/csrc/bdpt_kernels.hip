@@ -24,11 +24,26 @@ __device__ __forceinline__ f3 sub(f3 a, f3 b) { return mk(a.x - b.x, a.y - b.y, 
 __device__ __forceinline__ f3 mul(f3 a, f3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
 __device__ __forceinline__ f3 smul(float k, f3 b) { return mk(k * b.x, k * b.y, k * b.z); }
 __device__ __forceinline__ float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+// 1.f / x, correctly rounded: v_rcp_f32 + one Newton fma is exactly that for |x| in
+// [2^-125, 2^125) (all 2^32 inputs checked on gfx950 by tests/native/hw_exact_check.hip); other
+// x take the library division on an exec-masked branch.  rcp_rn_inrange: caller proves the range.
+__device__ __forceinline__ float rcp_rn_inrange(float x) {
+#ifdef BDPT_LIB_DIV
+    return 1.f / x;
+#endif
+    const float r = __builtin_amdgcn_rcpf(x);
+    return __builtin_fmaf(__builtin_fmaf(-x, r, 1.f), r, r);
+}
+__device__ __forceinline__ float rcp_rn(float x) {
+    const float ax = fabsf(x);
+    if (__builtin_expect(!(ax >= 0x1p-125f && ax < 0x1p125f), 0)) return 1.f / x;
+    return rcp_rn_inrange(x);
+}
 __device__ __forceinline__ f3 norm(f3 v) {
 #ifdef BDPT_ABL_DIV
     return smul(__builtin_amdgcn_rsqf(dot(v, v)), v);
 #endif
-    float l = 1.f / bdpt_sqrt_rn(dot(v, v)); return smul(l, v);
+    float l = rcp_rn(bdpt_sqrt_rn(dot(v, v))); return smul(l, v);
 }
 __device__ __forceinline__ f3 cross(f3 a, f3 b) {
     return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
@@ -103,7 +118,7 @@ __device__ __forceinline__ f3 cosine_dir(f3 w, float u_phi, float u_r2, const do
     const float r2s = bdpt_sqrt_rn_core(r2);                 // r2 = d_Rand value >= 2^-32
     f3 a = fabsf(w.x) > .1f ? mk(0.f, 1.f, 0.f) : mk(1.f, 0.f, 0.f);
     const f3 uc = cross(a, w);                                // |uc|^2 >= 0.01 by the choice of a
-    f3 u = smul(1.f / bdpt_sqrt_rn_core(dot(uc, uc)), uc);
+    f3 u = smul(rcp_rn_inrange(bdpt_sqrt_rn_core(dot(uc, uc))), uc);   // 0.1 <= |uc| <= 1
     f3 v = cross(w, u);
     float s, c;
     sincos_cr(r1, &s, &c, tab);
@@ -459,7 +474,7 @@ __global__ __launch_bounds__(256, N < 0 ? BDPT_BVH_WAVES : BDPT_WAVES_PER_SIMD) 
                 const float w = (c0.w * kx + c1.w * ky + c2.w * kz) + 1;
                 // (float)(1./(double)w) == 1.f/w: double rounding of a quotient is innocuous
                 // when 53 >= 2*24 + 2 (device.cu:594)
-                rdir = smul(1.f / w, rdir);
+                rdir = smul(rcp_rn(w), rdir);
                 ro = add(rdir, mk(c3.x, c3.y, c3.z));
                 rd = norm(rdir);
                 rad = mk(0.f, 0.f, 0.f);
@@ -584,7 +599,7 @@ __global__ __launch_bounds__(256, N < 0 ? BDPT_BVH_WAVES : BDPT_WAVES_PER_SIMD) 
                     const f3 spt = add(smul(lg.w, usp), mk(lg.x, lg.y, lg.z));
                     sd = sub(spt, ro);
                     const float len = bdpt_sqrt_rn(dot(sd, sd));
-                    sd = smul(1.f / len, sd);
+                    sd = smul(rcp_rn(len), sd);
                     float wo = dot(sd, usp);
                     if (!(wo > 0.f)) {
                         wo = -wo;
@@ -600,7 +615,7 @@ __global__ __launch_bounds__(256, N < 0 ? BDPT_BVH_WAVES : BDPT_WAVES_PER_SIMD) 
                     const float4 v0 = V[3 * p], v1 = V[3 * p + 1], v2 = V[3 * p + 2];
                     vsd = sub(mk(v0.x, v0.y, v0.z), ro);
                     const float len = bdpt_sqrt_rn(dot(vsd, vsd));
-                    vsd = smul(1.f / len, vsd);
+                    vsd = smul(rcp_rn(len), vsd);
                     float wo = dot(vsd, mk(v1.z, v1.w, v2.x));
                     if (!(wo > 0.f)) {
                         wo = -wo;
@@ -693,7 +708,7 @@ __global__ __launch_bounds__(256, N < 0 ? BDPT_BVH_WAVES : BDPT_WAVES_PER_SIMD) 
                         col = rad;
                     } else {
                         const float k1 = (float)cnt;
-                        const float k2 = 1.f / (k1 + 1.f);
+                        const float k2 = rcp_rn_inrange(k1 + 1.f);   // 2 <= k1+1 <= 30000
                         col.x = (col.x * k1 + rad.x) * k2;
                         col.y = (col.y * k1 + rad.y) * k2;
                         col.z = (col.z * k1 + rad.z) * k2;
