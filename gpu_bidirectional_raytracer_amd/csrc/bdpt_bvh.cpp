@@ -6,8 +6,8 @@
 // ever *skips* spheres that provably cannot change it (see DESIGN.md "Large scenes"):
 //   * spheres much larger than the typical one (the walls, r = 1e4 / 1e5) stay in a brute-force
 //     list -- they are hit by almost every ray and would swamp any bounding volume;
-//   * the others go into a binary BVH of axis-aligned boxes (median split on the widest
-//     centroid axis, <= 4 spheres per leaf), rounded outward to float;
+//   * the others go into a binary BVH of axis-aligned boxes (surface-area-heuristic splits,
+//     <= 4 spheres per leaf), rounded outward to float;
 //   * the tree is stored in depth-first order with a skip index per node ("threaded" BVH): a hit
 //     inner node continues at node+1 (its first child), a missed node or a finished leaf at its
 //     skip index, so a lane traverses without a stack;
@@ -43,6 +43,48 @@ struct builder {
         return (double)f < v ? std::nextafter(f, INFINITY) : f;
     }
 
+    static double area(const double lo[3], const double hi[3]) {
+        const double dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+        return dx * dy + dy * dz + dz * dx;
+    }
+
+    // Surface-area heuristic: over the three axes and every split of it[b, e) sorted by centroid,
+    // minimise area(left) * n_left + area(right) * n_right; leaves it[b, e) sorted along the chosen
+    // axis and returns the split index.  Ties keep the lowest axis / split (deterministic).
+    int split_sah(int b, int e) {
+        const int n = e - b;
+        double best = INFINITY;
+        int best_ax = 0, best_m = b + n / 2;
+        std::vector<double> right(n + 1);
+        for (int ax = 0; ax < 3; ax++) {
+            std::sort(it.begin() + b, it.begin() + e, [ax](const item& x, const item& y) {
+                return x.c[ax] < y.c[ax] || (x.c[ax] == y.c[ax] && x.id < y.id);
+            });
+            double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+            right[n] = 0.0;
+            for (int i = n - 1; i >= 1; i--) {
+                for (int a = 0; a < 3; a++) {
+                    lo[a] = std::min(lo[a], it[b + i].lo[a]);
+                    hi[a] = std::max(hi[a], it[b + i].hi[a]);
+                }
+                right[i] = area(lo, hi) * (n - i);
+            }
+            double llo[3] = {INFINITY, INFINITY, INFINITY}, lhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+            for (int i = 1; i < n; i++) {
+                for (int a = 0; a < 3; a++) {
+                    llo[a] = std::min(llo[a], it[b + i - 1].lo[a]);
+                    lhi[a] = std::max(lhi[a], it[b + i - 1].hi[a]);
+                }
+                const double cost = area(llo, lhi) * i + right[i];
+                if (cost < best) { best = cost; best_ax = ax; best_m = b + i; }
+            }
+        }
+        std::sort(it.begin() + b, it.begin() + e, [best_ax](const item& x, const item& y) {
+            return x.c[best_ax] < y.c[best_ax] || (x.c[best_ax] == y.c[best_ax] && x.id < y.id);
+        });
+        return best_m;
+    }
+
     // Emits the subtree of it[b, e) at nodes[2*k .. ], returns its node count.
     int build(int b, int e) {
         const int k = (int)nodes.size() / 2;
@@ -63,6 +105,7 @@ struct builder {
             for (int i = b; i < e; i++) order.push_back(it[i].id);
             nodes[2 * k + 1].w = bdpt_bits_as_float(first | ((e - b) << 24));
         } else {
+#ifdef BDPT_BVH_MEDIAN
             int ax = 0;
             for (int a = 1; a < 3; a++)
                 if (chi[a] - clo[a] > chi[ax] - clo[ax]) ax = a;
@@ -71,6 +114,9 @@ struct builder {
                              [ax](const item& x, const item& y) {
                                  return x.c[ax] < y.c[ax] || (x.c[ax] == y.c[ax] && x.id < y.id);
                              });
+#else
+            const int m = split_sah(b, e);
+#endif
             nodes[2 * k + 1].w = bdpt_bits_as_float(-1);
             count += build(b, m);
             count += build(m, e);
