@@ -102,7 +102,6 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    import numpy as np
     import torch
 
     import gpu_bidirectional_raytracer_amd as g

@@ -12,7 +12,7 @@ from __future__ import annotations
 
 import ctypes
 import os
-from typing import Iterable, Optional, Sequence, Tuple
+from typing import Optional, Sequence, Tuple
 
 import numpy as np
 

@@ -7,6 +7,8 @@
  * Plain C: no torch / HIP types in any signature.  All functions return 0 on success and a
  * negative BDPT_E* code on failure; the message is in bdpt_last_error() (the reference prints
  * cudaGetErrorString() and continues, smallpt_cpu.c:169-233 -- the host does the same with this).
+ * One context per GPU; calls on one context must not run concurrently (the reference is single-
+ * threaded too); different contexts are independent.
  *
  * Types are layout-compatible with the reference headers (static-asserted in the library):
  *   bdpt_vec       == Vec        include/vec.h:4-6       (12 B)

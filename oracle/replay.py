@@ -20,7 +20,7 @@ import ctypes
 
 import numpy as np
 
-from . import (CAMERA_DTYPE, RAND_N, SPHERE_DTYPE, key_camera, light_pass, mt607, path_passes,
+from . import (RAND_N, SPHERE_DTYPE, key_camera, light_pass, mt607, path_passes,
                special_key, update_camera)
 
 MAX_ITER = 3          # smallpt_cpu.c: flag cycles 2 -> 3 -> (vlp_index += MAX_VLP; 1 -> 2)
