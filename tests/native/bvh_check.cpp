@@ -86,6 +86,46 @@ void closest_bvh(const bdpt_bvh& B, v3 o, v3 d, float& t, int& id) {
     }
 }
 
+// Metrics only: closest hit with an explicit stack, nearer child first (by child-box centre
+// along the ray), to measure how much ordered traversal would save over the threaded walk.
+long g_onodes = 0, g_otests = 0;
+void closest_ordered(const bdpt_bvh& B, v3 o, v3 d, float& t, int& id) {
+    t = 1e20f;
+    id = -1;
+    for (int q = (int)B.big_geom.size() - 1; q >= 0; --q) {
+        const float dd = isect(B.big_geom[q], o, d);
+        const int s = B.big_ids[q] & (kBvhEmissive - 1);
+        if (dd < t || (dd == t && s > id)) { t = dd; id = s; }
+    }
+    const bvh_ray br = setup(B, o, d);
+    int stack[64], sp = 0;
+    stack[sp++] = 0;
+    while (sp) {
+        const int node = stack[--sp];
+        const float4 lo = B.nodes[2 * node], hi = B.nodes[2 * node + 1];
+        g_onodes++;
+        if (!box(lo, hi, br, t)) continue;
+        const int info = ibits(hi.w);
+        if (info >= 0) {
+            const int first = info & 0xffffff, end = first + (info >> 24);
+            for (int k = first; k < end; k++) {
+                const float dd = isect(B.geom[k], o, d);
+                const int s = B.ids[k] & (kBvhEmissive - 1);
+                g_otests++;
+                if (dd < t || (dd == t && s > id)) { t = dd; id = s; }
+            }
+            continue;
+        }
+        const int l = node + 1, r = ibits(B.nodes[2 * l].w);
+        auto centre = [&](int n) {
+            const float4 a = B.nodes[2 * n], b = B.nodes[2 * n + 1];
+            return (0.5f * (a.x + b.x) - o.x) * d.x + (0.5f * (a.y + b.y) - o.y) * d.y + (0.5f * (a.z + b.z) - o.z) * d.z;
+        };
+        if (centre(l) <= centre(r)) { stack[sp++] = r; stack[sp++] = l; }
+        else { stack[sp++] = l; stack[sp++] = r; }
+    }
+}
+
 bool occluded_bvh(const bdpt_bvh& B, v3 o, v3 d, float maxt, bool vac) {
     for (size_t q = 0; q < B.big_geom.size(); q++)
         if (isect(B.big_geom[q], o, d) < maxt && !(vac && (B.big_ids[q] & kBvhEmissive))) return true;
@@ -143,6 +183,8 @@ int main(int argc, char** argv) {
         int ib;
         closest_bvh(B, o, d, tb, ib);
         if (ibits(t) != ibits(tb) || id != ib) bad_closest++;
+        closest_ordered(B, o, d, tb, ib);
+        if (ibits(t) != ibits(tb) || id != ib) bad_closest++;
         // shadow ray from o to a random point (maxt random in [0, 1.2 t])
         const float maxt = U(rng) * 1.2f * (id >= 0 ? t : 300.f);
         const bool vac = (k & 1) != 0;
@@ -161,9 +203,10 @@ int main(int argc, char** argv) {
     }
     printf("{\"bvh\": true, \"nodes\": %zu, \"bvh_spheres\": %zu, \"walls\": %zu, \"rays\": %ld, "
            "\"bad_closest\": %ld, \"bad_shadow\": %ld, \"hits\": %ld, \"occluded\": %ld, "
-           "\"node_visits_per_ray\": %.2f, \"sphere_tests_per_ray\": %.2f}\n",
+           "\"node_visits_per_ray\": %.2f, \"sphere_tests_per_ray\": %.2f, "
+           "\"ordered_node_visits\": %.2f, \"ordered_sphere_tests\": %.2f}\n",
            B.nodes.size() / 2, B.geom.size(), B.big_geom.size(), nrays, bad_closest, bad_shadow, hits, occl,
-           (double)g_nodes / nrays, (double)g_tests / nrays);
+           (double)g_nodes / nrays, (double)g_tests / nrays, (double)g_onodes / nrays, (double)g_otests / nrays);
     free(sp);
     return bad_closest || bad_shadow ? 1 : 0;
 }
