@@ -18,7 +18,13 @@ LIB      ?= $(PKG)/libbdpt.so
 HOST     := $(PKG)/smallpt
 ORACLE   := oracle/liboracle.so
 
-all: $(LIB) $(HOST) $(ORACLE)
+CHECKS   := tests/native/hw_exact_check
+
+all: $(LIB) $(HOST) $(ORACLE) $(CHECKS)
+
+# exhaustive hardware checks run by tests/test_gpu_hw_exact.py (test infrastructure)
+tests/native/hw_exact_check: tests/native/hw_exact_check.hip $(CSRC)/bdpt_math.h
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -ffp-contract=off -o $@ $<
 
 $(BUILD):
 	mkdir -p $(BUILD)
@@ -46,7 +52,7 @@ $(ORACLE): oracle/bdpt_oracle.c include/bdpt.h
 	$(CC) -O2 -std=gnu11 -fPIC -shared -fopenmp -ffp-contract=off -Wall -o $@ $< -lm
 
 clean:
-	rm -rf $(BUILD) $(LIB) $(HOST) $(ORACLE)
+	rm -rf $(BUILD) $(LIB) $(HOST) $(ORACLE) $(CHECKS)
 
 # A/B variants for the GPU bench harness: make variant NAME=x EXTRA_HIPFLAGS="..."
 variant:

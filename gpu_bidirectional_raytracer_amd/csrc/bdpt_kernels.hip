@@ -89,7 +89,14 @@ __device__ __forceinline__ float sphere_isect(float4 g, f3 o, f3 d) {
 
 // The same test with "no hit" encoded as +inf instead of 0, so the closest-hit update is one
 // compare (d < t) and the any-hit test is d < maxt.  t1 > EPS ? t1 : (t2 > EPS ? t2 : miss) ==
-// (r = t1 > EPS ? t1 : t2) > EPS ? r : miss; det < 0 (or NaN) -> miss, as in the reference.
+// (r = t1 > EPS ? t1 : t2) > EPS ? r : miss.
+// The reference's `det < 0 -> miss` needs no test of its own (+2.7 % measured): a negative normal
+// det gives a NaN root (bdpt_sqrt_rn_core), so t1, t2, r are NaN and r > EPS fails; so does a
+// generated NaN det.  A negative denormal det may give a root of -0 (v_sqrt_f32 flushes it), so
+// r = b -- but then b <= EPS, a miss again: if b > EPS, then fl(b*b) >= 1e-4 and X = fl(b*b - oo)
+// is either > 0 (oo < b*b/2; then det >= X > 0) or a multiple of 2^-38 (ulp(oo) >= 2^-38), and
+// det = fl(X + r*r) is then >= 0, <= -2^-39, or a nonzero multiple of ulp(r*r) >= 2^-83 -- never
+// in (-2^-126, 0).  (det is never -0: fl(b*b) is not -0.)
 __device__ __forceinline__ float sphere_isect_inf(float4 g, f3 o, f3 d) {
     f3 op = mk(g.x - o.x, g.y - o.y, g.z - o.z);
     float b = dot(op, d);
@@ -97,7 +104,28 @@ __device__ __forceinline__ float sphere_isect_inf(float4 g, f3 o, f3 d) {
     const float s = bdpt_sqrt_rn_core(det);
     const float t1 = b - s, t2 = b + s;
     const float r = t1 > kEps ? t1 : t2;
-    return (r > kEps && det >= 0.f) ? r : __builtin_inff();
+    return r > kEps ? r : __builtin_inff();
+}
+
+// The same test as an unsigned key for the brute-force loops: k = bits(r) - bits(EPSILON) - 1 with
+// r = t1 > EPS ? t1 : t2 (a NaN when det < 0).  For a float r, "r > EPS && r < T" (the reference's
+// valid-and-closer test) is exactly k < bits(T) - bits(EPS) - 1 as unsigned integers whenever
+// EPS < T < inf: positive floats order like their bit patterns, and every r that is not a hit
+// (r <= EPS, -0, negative, NaN) maps to a key >= 2^31 - bits(EPS) > any such T's key.  One integer
+// compare replaces the float compare + inf select + compare of sphere_isect_inf.
+constexpr unsigned kEpsKey = 0x3c23d70bu;                  // bits(0.01f) + 1
+static_assert(__builtin_bit_cast(unsigned, kEps) + 1u == kEpsKey, "EPSILON key");
+__device__ __forceinline__ unsigned sphere_key(float4 g, f3 o, f3 d) {
+    f3 op = mk(g.x - o.x, g.y - o.y, g.z - o.z);
+    float b = dot(op, d);
+    float det = b * b - dot(op, op) + g.w;
+    const float s = bdpt_sqrt_rn_core(det);
+    const float t1 = b - s, t2 = b + s;
+    return __float_as_uint(t1 > kEps ? t1 : t2) - kEpsKey;
+}
+// key of an upper bound T (closest-hit distance or shadow maxt): 0 when T <= EPS (nothing hits)
+__device__ __forceinline__ unsigned dist_key(float T) {
+    return (unsigned)(max(__float_as_int(T), (int)kEpsKey) - (int)kEpsKey);
 }
 
 // UniformSampleSphereDevice device.cu:157-165
@@ -326,6 +354,9 @@ __device__ __forceinline__ bool bvh_box(float4 lo, float4 hi, const bvh_ray& r, 
 }
 }  // namespace
 
+#ifndef BDPT_ISECT_KEY
+#define BDPT_ISECT_KEY 0
+#endif
 #ifndef BDPT_WAVES_PER_SIMD
 #define BDPT_WAVES_PER_SIMD 5
 #endif
@@ -514,11 +545,21 @@ __global__ __launch_bounds__(256, N < 0 ? BDPT_BVH_WAVES : BDPT_WAVES_PER_SIMD) 
                     }
                 }
             } else {
+#if BDPT_ISECT_KEY
+                unsigned tk = dist_key(t);
+#pragma unroll kUnroll
+                for (int s = n - 1; s >= 0; --s) {
+                    const unsigned k = sphere_key(geom(s), ro, rd);
+                    if (k < tk) { tk = k; id = s; }
+                }
+                t = __uint_as_float(tk + kEpsKey);
+#else
 #pragma unroll kUnroll
                 for (int s = n - 1; s >= 0; --s) {
                     const float d = sphere_isect_inf(geom(s), ro, rd);
                     if (d < t) { t = d; id = s; }
                 }
+#endif
             }
             done = id < 0;
             if (!done) {
@@ -673,12 +714,22 @@ __global__ __launch_bounds__(256, N < 0 ? BDPT_BVH_WAVES : BDPT_WAVES_PER_SIMD) 
                                 node = occ ? a.bvh_nn : __float_as_int(lo.w);
                             }
                         } else {
+#if BDPT_ISECT_KEY
+                        const unsigned mk = dist_key(r0.w);
+#pragma unroll kUnroll
+                        for (int s = n - 1; s >= 0; --s) {                // IntersectP(Vacuum)Device
+                            const unsigned kk = sphere_key(geom(s), o, d);
+                            // early exit (measured +2% over a branch-free loop)
+                            if (kk < mk && !(vac && emissive(s))) { occ = 1; break; }
+                        }
+#else
 #pragma unroll kUnroll
                         for (int s = n - 1; s >= 0; --s) {                // IntersectP(Vacuum)Device
                             const float dd = sphere_isect_inf(geom(s), o, d);
                             // early exit (measured +2% over a branch-free loop)
                             if (dd < r0.w && !(vac && emissive(s))) { occ = 1; break; }
                         }
+#endif
                         }
                         SR[idx] = occ;
                     }

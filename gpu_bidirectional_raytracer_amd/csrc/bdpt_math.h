@@ -62,19 +62,50 @@ BDPT_HD void bdpt_sincos_tab(double x, const double* tab, double* so, double* co
     *co = fma(C, cr, -(S * sr));
 }
 
+#ifndef BDPT_SQRT_SHIFT
+#define BDPT_SQRT_SHIFT 1
+#endif
+#ifndef BDPT_SQRT_ONESIDED
+#define BDPT_SQRT_ONESIDED 0
+#endif
 #if defined(__HIPCC__)
 // v_sqrt_f32 + the +-1 ulp residual correction: correctly rounded for x >= 2^-96 and x == 0.
 __device__ __forceinline__ float bdpt_sqrt_rn_core(float x) {
 #ifdef BDPT_ABL_SQRT
     return __builtin_amdgcn_sqrtf(x);
 #endif
+#if BDPT_SQRT_SHIFT
+    // The same decision without VCC selects (+5 % on the path kernel with the det test dropped,
+    // bdpt_kernels.hip sphere_isect_inf): the residuals are taken with the opposite sign,
+    // r' = fl(s*n - x), so "x <= sdn*s" / "x > sup*s" are sign bits (an exact zero is +0 in
+    // round-to-nearest), and s = sdn + [x <= sdn*s is false] + [x > sup*s] (the two conditions
+    // exclude each other).  sdn saturates at 0 for s = +0 (then x = 0: both sign bits are 0).
+    // Checked against the select form and (float)sqrt((double)x) on all 2^32 inputs on gfx950
+    // (scripts/sqrt_shift_check.hip): equal for x = +0 and every x >= 2^-96; a NaN for negative
+    // normal x and generated (canonical) NaNs; a NaN or -0 for -0 and negative denormals.
+    {
+        const unsigned sb = __float_as_uint(__builtin_amdgcn_sqrtf(x));
+        const unsigned db = __builtin_elementwise_sub_sat(sb, 1u);
+        const float rdn = __builtin_fmaf(__uint_as_float(db), __uint_as_float(sb), -x);
+        const float rup = __builtin_fmaf(__uint_as_float(sb + 1u), __uint_as_float(sb), -x);
+        return __uint_as_float(db + (__float_as_uint(rdn) >> 31) + (__float_as_uint(rup) >> 31));
+    }
+#endif
     float s = __builtin_amdgcn_sqrtf(x);
     const float sdn = __int_as_float(__float_as_int(s) - 1);
     const float sup = __int_as_float(__float_as_int(s) + 1);
     const float rdn = __builtin_fmaf(-sdn, s, x);
     const float rup = __builtin_fmaf(-sup, s, x);
+#if BDPT_SQRT_ONESIDED == 1
+    (void)rdn;
+    s = rup > 0.f ? sup : s;
+#elif BDPT_SQRT_ONESIDED == 2
+    (void)rup;
+    s = rdn <= 0.f ? sdn : s;
+#else
     s = rdn <= 0.f ? sdn : s;
     s = rup > 0.f ? sup : s;
+#endif
     return s;
 }
 
