@@ -62,12 +62,16 @@ __device__ const double bdpt_sincos_table_dev[256][2] = BDPT_SINCOS_TABLE_INIT;
 #ifndef BDPT_SINCOS_TABLE
 #define BDPT_SINCOS_TABLE 1
 #endif
-__device__ __forceinline__ void sincos_cr(float x, float* s, float* c, const double* tab = nullptr) {
+// The choice is a template argument, not a null test on `tab`: the compiler cannot prove an
+// LDS-derived pointer non-null, and the dead minimax path then kept its fp64 coefficients in
+// ~20 VGPRs across the whole path loop.
+template <bool TAB>
+__device__ __forceinline__ void sincos_cr(float x, float* s, float* c, const double* tab) {
 #ifdef BDPT_ABL_SINCOS
     *s = __sinf(x); *c = __cosf(x); return;
 #endif
     double sd, cd;
-    if (BDPT_SINCOS_TABLE && tab) bdpt_sincos_tab((double)x, tab, &sd, &cd);
+    if constexpr (TAB && BDPT_SINCOS_TABLE) bdpt_sincos_tab((double)x, tab, &sd, &cd);
     else bdpt_sincos_dp((double)x, &sd, &cd);
     *s = (float)sd;
     *c = (float)cd;
@@ -129,17 +133,19 @@ __device__ __forceinline__ unsigned dist_key(float T) {
 }
 
 // UniformSampleSphereDevice device.cu:157-165
+template <bool TAB = false>
 __device__ __forceinline__ f3 uniform_sphere(float u1, float u2, const double* tab = nullptr) {
     const float zz = 1.f - 2.f * u1;
     const float q = 1.f - zz * zz;
     const float r = bdpt_sqrt_rn_core(0.f > q ? 0.f : q);   // q is 0 or >= 2^-24: core is exact
     const float phi = 2.f * kPi * u2;
     float s, c;
-    sincos_cr(phi, &s, &c, tab);
+    sincos_cr<TAB>(phi, &s, &c, tab);
     return mk(r * c, r * s, zz);
 }
 
 // Cosine-weighted direction about w (device.cu:676-699; also :190-212 and :357-380).
+template <bool TAB = false>
 __device__ __forceinline__ f3 cosine_dir(f3 w, float u_phi, float u_r2, const double* tab = nullptr) {
     const float r1 = 2.f * kPi * u_phi;
     const float r2 = u_r2;
@@ -149,7 +155,7 @@ __device__ __forceinline__ f3 cosine_dir(f3 w, float u_phi, float u_r2, const do
     f3 u = smul(rcp_rn_inrange(bdpt_sqrt_rn_core(dot(uc, uc))), uc);   // 0.1 <= |uc| <= 1
     f3 v = cross(w, u);
     float s, c;
-    sincos_cr(r1, &s, &c, tab);
+    sincos_cr<TAB>(r1, &s, &c, tab);
     u = smul(c * r2s, u);
     v = smul(s * r2s, v);
     f3 nd = add(u, v);
@@ -356,6 +362,9 @@ __device__ __forceinline__ bool bvh_box(float4 lo, float4 hi, const bvh_ray& r, 
 
 #ifndef BDPT_ISECT_KEY
 #define BDPT_ISECT_KEY 0
+#endif
+#ifndef BDPT_ANYHIT_MIN
+#define BDPT_ANYHIT_MIN 0
 #endif
 #ifndef BDPT_WAVES_PER_SIMD
 #define BDPT_WAVES_PER_SIMD 5
@@ -581,42 +590,39 @@ __global__ __launch_bounds__(256, N < 0 ? BDPT_BVH_WAVES : BDPT_WAVES_PER_SIMD) 
                     thr = mul(thr, mk(cm.x, cm.y, cm.z));
                     diff = true;                  // shadow rays: below, compacted over the wave
                     ro = hit;
-                    rd = cosine_dir(nl, q0, q1, SCT);
-                } else if ((mat & 255) == BDPT_DEV_SPEC) {               // :704-714
-                    specular = true;
-                    const f3 nd = sub(rd, smul(2.f * dot(normal, rd), normal));
-                    thr = mul(thr, mk(cm.x, cm.y, cm.z));
-                    ro = hit;
-                    rd = nd;
-                } else {                                                 // REFR / LITE :715-770
+                    rd = cosine_dir<true>(nl, q0, q1, SCT);
+                } else {
+                    // SPEC :704-714 and REFR / LITE :715-770 share the mirror direction (one
+                    // evaluation when a wave holds lanes of both kinds)
                     specular = true;
                     const f3 refl = sub(rd, smul(2.f * dot(normal, rd), normal));
-                    const bool into = dot(normal, nl) > 0;
-                    const float nc = 1.f, nt = 1.5f;
-                    const float nnt = into ? nc / nt : nt / nc;
-                    const float ddn = dot(rd, nl);
-                    const float cos2t = 1.f - nnt * nnt * (1.f - ddn * ddn);
-                    if (cos2t < 0.f) {
+                    if ((mat & 255) == BDPT_DEV_SPEC) {
                         thr = mul(thr, mk(cm.x, cm.y, cm.z));
                         rd = refl;
                     } else {
-                        // cos2t = 1 - X is 0 or >= 2^-24 (Sterbenz for X >= 1/2, else > 1/2)
-                        const float kq = (float)(into ? 1 : -1) * (ddn * nnt + bdpt_sqrt_rn_core(cos2t));
-                        const f3 td = norm(sub(smul(nnt, rd), smul(kq, normal)));
-                        const float aa = nt - nc, bb = nt + nc;
-                        const float R0 = aa * aa / (bb * bb);
-                        const float c = 1 - (into ? -ddn : dot(td, normal));
-                        const float Re = R0 + (1 - R0) * c * c * c * c * c;
-                        const float Tr = 1.f - Re;
-                        const float Pp = .25f + .5f * Re;
-                        const float RP = Re / Pp;
-                        const float TP = Tr / (1.f - Pp);
-                        if (q2 < Pp) {
-                            thr = mul(smul(RP, thr), mk(cm.x, cm.y, cm.z));
+                        const bool into = dot(normal, nl) > 0;
+                        const float nc = 1.f, nt = 1.5f;
+                        const float nnt = into ? nc / nt : nt / nc;
+                        const float ddn = dot(rd, nl);
+                        const float cos2t = 1.f - nnt * nnt * (1.f - ddn * ddn);
+                        if (cos2t < 0.f) {
+                            thr = mul(thr, mk(cm.x, cm.y, cm.z));
                             rd = refl;
                         } else {
-                            thr = mul(smul(TP, thr), mk(cm.x, cm.y, cm.z));
-                            rd = td;
+                            // cos2t = 1 - X is 0 or >= 2^-24 (Sterbenz for X >= 1/2, else > 1/2)
+                            const float kq = (float)(into ? 1 : -1) * (ddn * nnt + bdpt_sqrt_rn_core(cos2t));
+                            const f3 td = norm(sub(smul(nnt, rd), smul(kq, normal)));
+                            const float aa = nt - nc, bb = nt + nc;
+                            const float R0 = aa * aa / (bb * bb);
+                            const float c = 1 - (into ? -ddn : dot(td, normal));
+                            const float Re = R0 + (1 - R0) * c * c * c * c * c;
+                            const float Tr = 1.f - Re;
+                            const float Pp = .25f + .5f * Re;
+                            // RP = Re / P or TP = Tr / (1 - P): only the one the lane uses is divided
+                            const bool reflect = q2 < Pp;
+                            const float k = (reflect ? Re : Tr) / (reflect ? Pp : 1.f - Pp);
+                            thr = mul(smul(k, thr), mk(cm.x, cm.y, cm.z));
+                            rd = reflect ? refl : td;
                         }
                     }
                     ro = hit;
@@ -628,7 +634,7 @@ __global__ __launch_bounds__(256, N < 0 ? BDPT_BVH_WAVES : BDPT_WAVES_PER_SIMD) 
         // NEE towards every emitter (same d_Rand[j+3], d_Rand[j+4] for all) + 1 VLP, blended 1/2.
         if (__builtin_amdgcn_ballot_w64(diff) != 0) {
             f3 res = mk(0.f, 0.f, 0.f), usp = res, vsd = res, vcon = res;
-            if (diff) usp = uniform_sphere(q3, q4, SCT);
+            if (diff) usp = uniform_sphere<true>(q3, q4, SCT);
             const int nsteps = a.n_lights > 0 ? (int)a.n_lights : 1;
             for (int li = 0; li < nsteps; li++) {                         // uniform
                 bool has_nee = false, has_vlp = false;
@@ -654,17 +660,22 @@ __global__ __launch_bounds__(256, N < 0 ? BDPT_BVH_WAVES : BDPT_WAVES_PER_SIMD) 
                 }
                 if (diff && li == 0) {                                    // the VLP (:507-537)
                     const float4 v0 = V[3 * p], v1 = V[3 * p + 1], v2 = V[3 * p + 2];
-                    vsd = sub(mk(v0.x, v0.y, v0.z), ro);
-                    const float len = bdpt_sqrt_rn(dot(vsd, vsd));
-                    vsd = smul(rcp_rn(len), vsd);
-                    float wo = dot(vsd, mk(v1.z, v1.w, v2.x));
-                    if (!(wo > 0.f)) {
-                        wo = -wo;
-                        const float wi = dot(vsd, nl);
-                        if (wi > 0.f) {
-                            has_vlp = true;
-                            vmaxt = len - kEps;
-                            vcon = smul(wi * wo, mk(v0.w, v1.x, v1.y));
+                    // a VLP with zero radiance adds exactly +0 to vres whether it is visible or
+                    // not (wi * wo is finite): no ray.  Wave-uniform under pass streams, where a
+                    // workgroup renders one pass (zero VLPs: cornell 6 %, cornell_glass 45 %)
+                    if (!(v0.w == 0.f && v1.x == 0.f && v1.y == 0.f)) {
+                        vsd = sub(mk(v0.x, v0.y, v0.z), ro);
+                        const float len = bdpt_sqrt_rn(dot(vsd, vsd));
+                        vsd = smul(rcp_rn(len), vsd);
+                        float wo = dot(vsd, mk(v1.z, v1.w, v2.x));
+                        if (!(wo > 0.f)) {
+                            wo = -wo;
+                            const float wi = dot(vsd, nl);
+                            if (wi > 0.f) {
+                                has_vlp = true;
+                                vmaxt = len - kEps;
+                                vcon = smul(wi * wo, mk(v0.w, v1.x, v1.y));
+                            }
                         }
                     }
                 }
@@ -714,7 +725,18 @@ __global__ __launch_bounds__(256, N < 0 ? BDPT_BVH_WAVES : BDPT_WAVES_PER_SIMD) 
                                 node = occ ? a.bvh_nn : __float_as_int(lo.w);
                             }
                         } else {
-#if BDPT_ISECT_KEY
+#if BDPT_ANYHIT_MIN
+                        // any hit as a minimum: blocked iff the smallest key over the spheres that
+                        // may block this ray is below maxt's (IntersectPVacuumDevice skips
+                        // emitters) -- no per-sphere exit branch, no VCC selects
+                        unsigned m_n = 0xffffffffu, m_e = 0xffffffffu;
+#pragma unroll kUnroll
+                        for (int s = n - 1; s >= 0; --s) {
+                            const unsigned kk = sphere_key(geom(s), o, d);
+                            if (emissive(s)) m_e = min(m_e, kk); else m_n = min(m_n, kk);
+                        }
+                        occ = min(m_n, vac ? 0xffffffffu : m_e) < dist_key(r0.w);
+#elif BDPT_ISECT_KEY
                         const unsigned mk = dist_key(r0.w);
 #pragma unroll kUnroll
                         for (int s = n - 1; s >= 0; --s) {                // IntersectP(Vacuum)Device
