@@ -111,27 +111,6 @@ __device__ __forceinline__ float sphere_isect_inf(float4 g, f3 o, f3 d) {
     return r > kEps ? r : __builtin_inff();
 }
 
-// The same test as an unsigned key for the brute-force loops: k = bits(r) - bits(EPSILON) - 1 with
-// r = t1 > EPS ? t1 : t2 (a NaN when det < 0).  For a float r, "r > EPS && r < T" (the reference's
-// valid-and-closer test) is exactly k < bits(T) - bits(EPS) - 1 as unsigned integers whenever
-// EPS < T < inf: positive floats order like their bit patterns, and every r that is not a hit
-// (r <= EPS, -0, negative, NaN) maps to a key >= 2^31 - bits(EPS) > any such T's key.  One integer
-// compare replaces the float compare + inf select + compare of sphere_isect_inf.
-constexpr unsigned kEpsKey = 0x3c23d70bu;                  // bits(0.01f) + 1
-static_assert(__builtin_bit_cast(unsigned, kEps) + 1u == kEpsKey, "EPSILON key");
-__device__ __forceinline__ unsigned sphere_key(float4 g, f3 o, f3 d) {
-    f3 op = mk(g.x - o.x, g.y - o.y, g.z - o.z);
-    float b = dot(op, d);
-    float det = b * b - dot(op, op) + g.w;
-    const float s = bdpt_sqrt_rn_core(det);
-    const float t1 = b - s, t2 = b + s;
-    return __float_as_uint(t1 > kEps ? t1 : t2) - kEpsKey;
-}
-// key of an upper bound T (closest-hit distance or shadow maxt): 0 when T <= EPS (nothing hits)
-__device__ __forceinline__ unsigned dist_key(float T) {
-    return (unsigned)(max(__float_as_int(T), (int)kEpsKey) - (int)kEpsKey);
-}
-
 // UniformSampleSphereDevice device.cu:157-165
 template <bool TAB = false>
 __device__ __forceinline__ f3 uniform_sphere(float u1, float u2, const double* tab = nullptr) {
@@ -360,11 +339,19 @@ __device__ __forceinline__ bool bvh_box(float4 lo, float4 hi, const bvh_ray& r, 
 }
 }  // namespace
 
-#ifndef BDPT_ISECT_KEY
-#define BDPT_ISECT_KEY 0
-#endif
-#ifndef BDPT_ANYHIT_MIN
-#define BDPT_ANYHIT_MIN 0
+#ifdef BDPT_STATS
+// instrumentation builds only (make variant NAME=stats EXTRA_HIPFLAGS=-DBDPT_STATS; read by
+// scripts/shadow_stats.py): [0] shadow steps, [1] shadow rounds, [2] shadow rays, [3] diffuse
+// lanes at shadow steps, [4] wave segments, [5] alive lanes at segment starts
+__device__ unsigned long long bdpt_dev_stats[8];
+extern "C" int bdpt_debug_stats(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(bdpt_dev_stats), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
+    if (reset) {
+        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(bdpt_dev_stats), z, sizeof z) != hipSuccess) return -1;
+    }
+    return 0;
+}
 #endif
 #ifndef BDPT_WAVES_PER_SIMD
 #define BDPT_WAVES_PER_SIMD 5
@@ -440,13 +427,11 @@ __global__ __launch_bounds__(256, N < 0 ? BDPT_BVH_WAVES : BDPT_WAVES_PER_SIMD) 
         K[3] = make_float4(a.orig[0], a.orig[1], a.orig[2], 0.f);
         K[4] = make_float4(a.inv_w, a.inv_h, 0.f, 0.f);
     }
-    // {sin, cos}(k pi/128) for the table-driven sincos (bdpt_math.h), 4 KB, one entry per thread
-    __shared__ double2 sct[256];
-    {
-        const double* t = &bdpt_sincos_table_dev[0][0];
-        sct[threadIdx.x] = make_double2(t[2 * threadIdx.x], t[2 * threadIdx.x + 1]);
-    }
-    const double* SCT = (const double*)sct;
+    // sin(k pi/128) for the table-driven sincos (bdpt_math.h; cos(k pi/128) is entry k + 64),
+    // 2 KB, one entry per thread
+    __shared__ double sct[256];
+    sct[threadIdx.x] = bdpt_sincos_table_dev[threadIdx.x][0];
+    const double* SCT = sct;
     __syncthreads();
 
     auto geom = [&](int s) -> float4 {
@@ -499,6 +484,15 @@ __global__ __launch_bounds__(256, N < 0 ? BDPT_BVH_WAVES : BDPT_WAVES_PER_SIMD) 
     bool alive = active && p < a.npass && cnt0 + (unsigned)p < BDPT_DEV_COUNTER_CAP;
 
     while (__builtin_amdgcn_ballot_w64(alive) != 0) {                   // wave-uniform loop
+#ifdef BDPT_STATS
+        {
+            const unsigned long long ma = __builtin_amdgcn_ballot_w64(alive);
+            if (lane == 0) {
+                atomicAdd(&bdpt_dev_stats[4], 1ull);
+                atomicAdd(&bdpt_dev_stats[5], (unsigned long long)__popcll(ma));
+            }
+        }
+#endif
         bool done = false, diff = false;
         if (alive) {
             if (fresh) {                  // camera ray (:562-600); d_Rand[kk] == q0 (kk == j)
@@ -554,21 +548,11 @@ __global__ __launch_bounds__(256, N < 0 ? BDPT_BVH_WAVES : BDPT_WAVES_PER_SIMD) 
                     }
                 }
             } else {
-#if BDPT_ISECT_KEY
-                unsigned tk = dist_key(t);
-#pragma unroll kUnroll
-                for (int s = n - 1; s >= 0; --s) {
-                    const unsigned k = sphere_key(geom(s), ro, rd);
-                    if (k < tk) { tk = k; id = s; }
-                }
-                t = __uint_as_float(tk + kEpsKey);
-#else
 #pragma unroll kUnroll
                 for (int s = n - 1; s >= 0; --s) {
                     const float d = sphere_isect_inf(geom(s), ro, rd);
                     if (d < t) { t = d; id = s; }
                 }
-#endif
             }
             done = id < 0;
             if (!done) {
@@ -694,6 +678,17 @@ __global__ __launch_bounds__(256, N < 0 ? BDPT_BVH_WAVES : BDPT_WAVES_PER_SIMD) 
                     SQ[kQueue + pv] = make_float4(vsd.x, vsd.y, vsd.z, 1.f);
                 }
                 wave_lds_fence();
+#ifdef BDPT_STATS
+                {
+                    const unsigned long long md = __builtin_amdgcn_ballot_w64(diff);
+                    if (lane == 0) {
+                        atomicAdd(&bdpt_dev_stats[0], 1ull);
+                        atomicAdd(&bdpt_dev_stats[1], (unsigned long long)((total + 63) / 64));
+                        atomicAdd(&bdpt_dev_stats[2], (unsigned long long)total);
+                        atomicAdd(&bdpt_dev_stats[3], (unsigned long long)__popcll(md));
+                    }
+                }
+#endif
                 for (int base = 0; base < total; base += 64) {            // uniform
                     const int idx = base + lane;
                     if (idx < total) {
@@ -725,33 +720,13 @@ __global__ __launch_bounds__(256, N < 0 ? BDPT_BVH_WAVES : BDPT_WAVES_PER_SIMD) 
                                 node = occ ? a.bvh_nn : __float_as_int(lo.w);
                             }
                         } else {
-#if BDPT_ANYHIT_MIN
-                        // any hit as a minimum: blocked iff the smallest key over the spheres that
-                        // may block this ray is below maxt's (IntersectPVacuumDevice skips
-                        // emitters) -- no per-sphere exit branch, no VCC selects
-                        unsigned m_n = 0xffffffffu, m_e = 0xffffffffu;
-#pragma unroll kUnroll
-                        for (int s = n - 1; s >= 0; --s) {
-                            const unsigned kk = sphere_key(geom(s), o, d);
-                            if (emissive(s)) m_e = min(m_e, kk); else m_n = min(m_n, kk);
-                        }
-                        occ = min(m_n, vac ? 0xffffffffu : m_e) < dist_key(r0.w);
-#elif BDPT_ISECT_KEY
-                        const unsigned mk = dist_key(r0.w);
-#pragma unroll kUnroll
-                        for (int s = n - 1; s >= 0; --s) {                // IntersectP(Vacuum)Device
-                            const unsigned kk = sphere_key(geom(s), o, d);
-                            // early exit (measured +2% over a branch-free loop)
-                            if (kk < mk && !(vac && emissive(s))) { occ = 1; break; }
-                        }
-#else
 #pragma unroll kUnroll
                         for (int s = n - 1; s >= 0; --s) {                // IntersectP(Vacuum)Device
                             const float dd = sphere_isect_inf(geom(s), o, d);
-                            // early exit (measured +2% over a branch-free loop)
+                            // early exit (measured +2% over a branch-free loop, +9% over a
+                            // branch-free running minimum of integer-keyed distances)
                             if (dd < r0.w && !(vac && emissive(s))) { occ = 1; break; }
                         }
-#endif
                         }
                         SR[idx] = occ;
                     }

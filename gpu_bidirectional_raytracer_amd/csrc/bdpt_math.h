@@ -47,17 +47,19 @@ BDPT_HD void bdpt_sincos_dp(double x, double* so, double* co) {
 
 // Table-driven fp64 sin & cos, cheaper than bdpt_sincos_dp (no quadrant logic, shorter
 // polynomials): k = rint(x * 128/pi), r = x - k*pi/128 (two-part constant, |r| <= pi/256),
-// sin x = S_k cos r + C_k sin r, cos x = C_k cos r - S_k sin r with {S_k, C_k} = tab[2k, 2k+1]
-// (bdpt_sincos_table.h, correctly rounded; the four axis entries exact).  For 0 <= x <= 2pi
-// (the render path's x = 2pi u).  Same exhaustive check as bdpt_sincos_dp (tests/test_math.py).
-BDPT_HD void bdpt_sincos_tab(double x, const double* tab, double* so, double* co) {
+// sin x = S_k cos r + C_k sin r, cos x = C_k cos r - S_k sin r with S_k = sintab[k] =
+// sin(k pi/128) and C_k = cos(k pi/128) = sintab[(k + 64) mod 256] (bdpt_sincos_table.h,
+// correctly rounded, so the two are the same double; the four axis entries exact).  For
+// 0 <= x <= 2pi (the render path's x = 2pi u).  Same exhaustive check as bdpt_sincos_dp
+// (tests/test_math.py).
+BDPT_HD void bdpt_sincos_tab(double x, const double* sintab, double* so, double* co) {
     const double kd = rint(x * BDPT_SC_INV);
     const int k = ((int)kd) & 255;                    // k = 256 is x = 2pi: entry 0
     const double r = fma(-kd, BDPT_SC_C2, fma(-kd, BDPT_SC_C1, x));
     const double z = r * r;
     const double sr = fma(r * z, fma(z, fma(z, -1.0 / 5040.0, 1.0 / 120.0), -1.0 / 6.0), r);
     const double cr = fma(z, fma(z, fma(z, -1.0 / 720.0, 1.0 / 24.0), -0.5), 1.0);
-    const double S = tab[2 * k], C = tab[2 * k + 1];
+    const double S = sintab[k], C = sintab[(k + 64) & 255];
     *so = fma(S, cr, C * sr);
     *co = fma(C, cr, -(S * sr));
 }

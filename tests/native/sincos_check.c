@@ -18,6 +18,8 @@ int main(int argc, char **argv)
     memcpy(&b0, &lo, 4);
     memcpy(&b1, &hi, 4);
     static const double tab[256][2] = BDPT_SINCOS_TABLE_INIT;
+    double sintab[256];                     /* the device's LDS copy: sin(k pi/128) only */
+    for (int k = 0; k < 256; k++) sintab[k] = tab[k][0];
     long n = 0, bad = 0, bad_tab = 0;
     for (uint64_t b = b0; b <= b1; b += stride) {
         uint32_t bb = (uint32_t)b;
@@ -32,7 +34,7 @@ int main(int argc, char **argv)
             if (bad < 5) printf("mismatch u=%a x=%a\n", u, x);
             bad++;
         }
-        bdpt_sincos_tab((double)x, &tab[0][0], &s, &c);
+        bdpt_sincos_tab((double)x, sintab, &s, &c);
         if ((float)s != gs || (float)c != gc) {
             if (bad_tab < 5) printf("table mismatch u=%a x=%a\n", u, x);
             bad_tab++;
