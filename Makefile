@@ -32,7 +32,11 @@ $(BUILD):
 $(BUILD)/bdpt_kernels.o: $(CSRC)/bdpt_kernels.hip $(CSRC)/bdpt_device.h $(CSRC)/bdpt_math.h $(CSRC)/bdpt_sincos_table.h | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(BUILD)/bdpt_host.o: $(CSRC)/bdpt_host.cpp $(CSRC)/bdpt_device.h $(CSRC)/bdpt_bvh.h include/bdpt.h | $(BUILD)
+# the path kernel's sources as strings, for scene-specialised kernels compiled at run time
+$(CSRC)/bdpt_jit_src.h: tools/embed_jit_sources.py $(CSRC)/bdpt_kernels.hip $(CSRC)/bdpt_device.h $(CSRC)/bdpt_math.h $(CSRC)/bdpt_sincos_table.h
+	python3 tools/embed_jit_sources.py $@
+
+$(BUILD)/bdpt_host.o: $(CSRC)/bdpt_host.cpp $(CSRC)/bdpt_device.h $(CSRC)/bdpt_bvh.h $(CSRC)/bdpt_jit_src.h include/bdpt.h | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(BUILD)/bdpt_bvh.o: $(CSRC)/bdpt_bvh.cpp $(CSRC)/bdpt_bvh.h include/bdpt.h | $(BUILD)
@@ -43,7 +47,7 @@ $(BUILD)/bdpt_util.o: $(CSRC)/bdpt_util.c include/bdpt.h | $(BUILD)
 
 $(LIB): $(BUILD)/bdpt_kernels.o $(BUILD)/bdpt_host.o $(BUILD)/bdpt_bvh.o $(BUILD)/bdpt_util.o
 	mkdir -p $(dir $(LIB))
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lm
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lm -ldl
 
 $(HOST): $(CSRC)/smallpt.c include/bdpt.h $(LIB)
 	$(CC) $(CFLAGS) -o $@ $< -L$(PKG) -lbdpt -lm -Wl,-rpath,'$$ORIGIN'
@@ -52,7 +56,7 @@ $(ORACLE): oracle/bdpt_oracle.c include/bdpt.h
 	$(CC) -O2 -std=gnu11 -fPIC -shared -fopenmp -ffp-contract=off -Wall -o $@ $< -lm
 
 clean:
-	rm -rf $(BUILD) $(LIB) $(HOST) $(ORACLE) $(CHECKS)
+	rm -rf $(BUILD) $(LIB) $(HOST) $(ORACLE) $(CHECKS) $(CSRC)/bdpt_jit_src.h
 
 # A/B variants for the GPU bench harness: make variant NAME=x EXTRA_HIPFLAGS="..."
 variant:

@@ -93,6 +93,8 @@ def main():
     ap.add_argument("--traversal", default="auto", choices=["auto", "brute", "bvh"],
                     help="sphere traversal for >16-sphere scenes (results identical)")
     ap.add_argument("--streams", type=int, default=0, help="pass streams per pixel (0 = auto)")
+    ap.add_argument("--specialize", type=int, default=1, choices=[0, 1],
+                    help="scene-specialised kernels (run-time compiled; results identical)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--rehearse", action="store_true",
@@ -125,6 +127,7 @@ def main():
     r.set_shard(rank, world, args.band_rows)
     r.set_traversal(args.traversal)
     r.set_streams(args.streams)
+    r.set_specialize(bool(args.specialize))
     r.light_pass(0)                                           # UpdateRendering2
     sched = g.PassScheduler()
     sched.light()
@@ -195,6 +198,7 @@ def main():
                 rec = json.load(open(pmc))
                 if rec.get("scene") == args.scene and rec.get("passes_per_launch") == passes_per_launch \
                         and rec.get("pass_streams") in (None, r.last_streams) \
+                        and rec.get("specialized", False) == r.last_specialized \
                         and rec.get("width") == W and rec.get("height") == H and world == 1:
                     traffic = rec.get("hbm_bytes_per_launch")
             roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
@@ -212,7 +216,8 @@ def main():
             if os.path.exists(pv) and world == 1:
                 rec = json.load(open(pv))
                 if rec.get("scene") == args.scene and rec.get("passes_per_launch") == passes_per_launch \
-                        and rec.get("pass_streams") == r.last_streams and rec.get("width") == W:
+                        and rec.get("pass_streams") == r.last_streams and rec.get("width") == W \
+                        and rec.get("specialized", False) == r.last_specialized:
                     valu["busy_pmc"] = rec["valu_busy"]
                     valu["lane_utilisation_pmc"] = rec["valu_lane_utilisation"]
             if r.last_traversal == "bvh":
@@ -231,7 +236,8 @@ def main():
                        "scene": args.scene, "width": W, "height": H, "passes_per_step": per_step,
                        "spp_total": per_step * (args.warmup + args.steps),
                        "parallelism": f"pixel bands x{world} ({args.band_rows}-row, interleaved)",
-                       "pass_streams": r.last_streams, "traversal": r.last_traversal},
+                       "pass_streams": r.last_streams, "traversal": r.last_traversal,
+                       "specialized": r.last_specialized},
             "device_ms_per_step": round(dev_ms / args.steps, 3),
             "roofline": roofline, "valu": valu, "cpu_baseline": cpu,
         }

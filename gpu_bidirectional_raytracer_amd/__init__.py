@@ -215,6 +215,19 @@ class Renderer:
     def last_streams(self) -> int:
         return int(lib.bdpt_last_streams(self._h))
 
+    def set_specialize(self, on: bool) -> None:
+        """Scene-specialised kernels (run-time compiled, <= 32 spheres); results are bit-identical."""
+        self._chk(lib.bdpt_set_specialize(self._h, int(bool(on))))
+
+    @property
+    def last_specialized(self) -> bool:
+        return bool(lib.bdpt_last_specialized(self._h))
+
+    @property
+    def specialize_status(self) -> str:
+        """Why the last path pass did not run a specialised kernel ('' if it did or was not asked)."""
+        return lib.bdpt_specialize_status(self._h).decode()
+
     def set_traversal(self, mode: str) -> None:
         """'auto' (BVH when the scene has one), 'brute' (every sphere) or 'bvh'."""
         self._chk(lib.bdpt_set_traversal(self._h, {"auto": 0, "brute": 1, "bvh": 2}[mode]))

@@ -69,6 +69,9 @@ _SIGS = [
     ("bdpt_set_shard", ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     ("bdpt_set_streams", ctypes.c_int, [_P, ctypes.c_int]),
     ("bdpt_last_streams", ctypes.c_int, [_P]),
+    ("bdpt_set_specialize", ctypes.c_int, [_P, ctypes.c_int]),
+    ("bdpt_last_specialized", ctypes.c_int, [_P]),
+    ("bdpt_specialize_status", ctypes.c_char_p, [_P]),
     ("bdpt_set_traversal", ctypes.c_int, [_P, ctypes.c_int]),
     ("bdpt_kernel_timing", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong), ctypes.c_int]),
     ("bdpt_scene_has_bvh", ctypes.c_int, [_P]),

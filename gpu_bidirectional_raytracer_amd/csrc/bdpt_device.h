@@ -10,7 +10,9 @@
 #ifndef BDPT_DEVICE_H
 #define BDPT_DEVICE_H
 
+#ifndef __HIPCC_RTC__                       // hipRTC provides the HIP runtime itself
 #include <hip/hip_runtime.h>
+#endif
 
 #define BDPT_DEV_RAND_N (4096u * 1876u)
 #define BDPT_DEV_N_PER_RNG 1876

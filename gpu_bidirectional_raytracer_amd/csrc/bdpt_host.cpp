@@ -5,12 +5,18 @@
 // loadMTGPU/seedMTGPU of src/MersenneTwister_kernel.cu:23-51.  One context = one GPU + one
 // HIP stream.  Every HIP call is checked; failures return BDPT_EHIP with the HIP message in
 // bdpt_last_error() (the reference prints and continues; the host shell decides).
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <hip/hiprtc.h>
 #include <math.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/stat.h>
+#include <unistd.h>
+#include <map>
+#include <string>
 #include <vector>
 
 #include "../../include/bdpt.h"
@@ -92,6 +98,12 @@ struct bdpt_ctx {
     float* d_thr = nullptr;
     int pass_cap = 0;
     uint32_t h_params[4 * BDPT_MT_RNG_COUNT];
+    // scene-specialised path kernels (hipRTC), by compile options; modules live until destroy
+    bool specialize = true;             // bdpt_set_specialize
+    bool last_specialized = false;
+    std::map<std::string, hipFunction_t> jit_fns;
+    std::vector<hipModule_t> jit_mods;
+    char jit_err[256] = {0};            // why the last specialisation fell back (diagnostics)
     char err[512] = {0};
 };
 
@@ -216,7 +228,194 @@ static void release(bdpt_ctx* c) {
         if (s.ev1) (void)hipEventDestroy(s.ev1);
     }
     if (c->h_pass) (void)hipHostFree(c->h_pass);
+    for (hipModule_t m : c->jit_mods) (void)hipModuleUnload(m);
     if (c->stream) (void)hipStreamDestroy(c->stream);
+}
+
+// ---- scene-specialised path kernels (run-time compiled with hipRTC) -------------------------
+// For scenes of <= 32 spheres (not BVH-traversed) the path kernel is recompiled with the scene folded in
+// (bdpt_kernels.hip BDPT_JIT): the sphere geometry {p, rad^2} as exact hex-float literals and the
+// emitter mask become compile-time constants, so a coordinate difference p - o that several
+// spheres share is formed once per ray (cornell's 9 spheres have 15 distinct coordinates, not
+// 27) and the scalar scene loads go away: +7 % on cornell.  The float operations are the same in
+// the same order, so results are bit-identical to the precompiled kernels
+// (tests/test_gpu_specialize.py).  hipRTC is opened with dlopen; when it is missing or a compile
+// fails, the precompiled instance runs (bdpt_last_specialized() says which one did).  Code objects
+// are cached per context and on disk ($BDPT_JIT_CACHE, else $HOME/.cache/bdpt-jit, else /tmp),
+// keyed by a hash of the sources and options; a compile takes ~1 s.
+#include "bdpt_jit_src.h"
+
+namespace {
+struct rtc_api {
+    bool ok = false;
+    decltype(&hiprtcCreateProgram) create = nullptr;
+    decltype(&hiprtcAddNameExpression) add_name = nullptr;
+    decltype(&hiprtcCompileProgram) compile = nullptr;
+    decltype(&hiprtcGetLoweredName) lowered = nullptr;
+    decltype(&hiprtcGetCodeSize) code_size = nullptr;
+    decltype(&hiprtcGetCode) code = nullptr;
+    decltype(&hiprtcGetProgramLogSize) log_size = nullptr;
+    decltype(&hiprtcGetProgramLog) log = nullptr;
+    decltype(&hiprtcDestroyProgram) destroy = nullptr;
+};
+
+const rtc_api& rtc() {
+    static const rtc_api api = [] {
+        rtc_api r;
+        const char* libs[] = {"libhiprtc.so.7", "libhiprtc.so", "/opt/rocm/lib/libhiprtc.so.7",
+                              "/opt/rocm/lib/libhiprtc.so"};
+        void* h = nullptr;
+        for (const char* l : libs)
+            if ((h = dlopen(l, RTLD_NOW | RTLD_LOCAL))) break;
+        if (!h) return r;
+#define BDPT_RTC_SYM(f, n) r.f = (decltype(r.f))dlsym(h, n)
+        BDPT_RTC_SYM(create, "hiprtcCreateProgram");
+        BDPT_RTC_SYM(add_name, "hiprtcAddNameExpression");
+        BDPT_RTC_SYM(compile, "hiprtcCompileProgram");
+        BDPT_RTC_SYM(lowered, "hiprtcGetLoweredName");
+        BDPT_RTC_SYM(code_size, "hiprtcGetCodeSize");
+        BDPT_RTC_SYM(code, "hiprtcGetCode");
+        BDPT_RTC_SYM(log_size, "hiprtcGetProgramLogSize");
+        BDPT_RTC_SYM(log, "hiprtcGetProgramLog");
+        BDPT_RTC_SYM(destroy, "hiprtcDestroyProgram");
+#undef BDPT_RTC_SYM
+        r.ok = r.create && r.add_name && r.compile && r.lowered && r.code_size && r.code &&
+               r.log_size && r.log && r.destroy;
+        return r;
+    }();
+    return api;
+}
+
+uint64_t fnv1a(uint64_t h, const void* p, size_t n) {
+    const unsigned char* b = (const unsigned char*)p;
+    for (size_t i = 0; i < n; i++) h = (h ^ b[i]) * 1099511628211ull;
+    return h;
+}
+
+std::string hexf(float v) {                     // exact float literal
+    char b[48];
+    snprintf(b, sizeof b, "%af", (double)v);
+    return b;
+}
+
+std::string jit_cache_dir() {
+    if (const char* d = getenv("BDPT_JIT_CACHE")) return d;
+    if (const char* home = getenv("HOME")) return std::string(home) + "/.cache/bdpt-jit";
+    return "/tmp/bdpt-jit-" + std::to_string((long)getuid());
+}
+
+bool read_file(const std::string& path, std::vector<char>& out) {
+    FILE* f = fopen(path.c_str(), "rb");
+    if (!f) return false;
+    fseek(f, 0, SEEK_END);
+    const long n = ftell(f);
+    fseek(f, 0, SEEK_SET);
+    out.resize(n > 0 ? (size_t)n : 0);
+    const bool ok = n > 0 && fread(out.data(), 1, (size_t)n, f) == (size_t)n;
+    fclose(f);
+    return ok;
+}
+
+void write_file_atomic(const std::string& dir, const std::string& path, const std::vector<char>& data) {
+    std::string d;                                           // mkdir -p
+    for (size_t i = 0; i <= dir.size(); i++) {
+        if (i == dir.size() || dir[i] == '/') {
+            if (!d.empty()) mkdir(d.c_str(), 0755);
+        }
+        if (i < dir.size()) d += dir[i];
+    }
+    const std::string tmp = path + ".tmp." + std::to_string((long)getpid());
+    FILE* f = fopen(tmp.c_str(), "wb");
+    if (!f) return;
+    const bool ok = fwrite(data.data(), 1, data.size(), f) == data.size();
+    fclose(f);
+    if (ok) rename(tmp.c_str(), path.c_str()); else unlink(tmp.c_str());
+}
+}  // namespace
+
+// The specialised kernel for the context's scene and pass-stream mode, compiled on first use;
+// nullptr = use the precompiled instance (reason in c->jit_err).
+static hipFunction_t jit_path_kernel(bdpt_ctx* c, bool streams) {
+    const unsigned n = (unsigned)c->spheres.size();
+    if (!c->specialize || n < 1 || n > 32) return nullptr;          // kJitEmis is 32 bits
+    const rtc_api& api = rtc();
+    if (!api.ok) {
+        snprintf(c->jit_err, sizeof c->jit_err, "hipRTC not found");
+        return nullptr;
+    }
+    std::string geom = "{";
+    for (unsigned i = 0; i < n; i++) {
+        const bdpt_sphere& sp = c->spheres[i];
+        const float rr = sp.rad * sp.rad;                    // as upload_scene forms it
+        geom += (i ? ",{" : "{") + hexf(sp.p.x) + "," + hexf(sp.p.y) + "," + hexf(sp.p.z) + "," + hexf(rr) + "}";
+    }
+    geom += "}";
+    const char* waves = getenv("BDPT_JIT_WAVES");
+    std::vector<std::string> opts = {
+        "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize",
+        "-fno-gpu-flush-denormals-to-zero", "-DBDPT_JIT=1", "-DBDPT_JIT_N=" + std::to_string(n),
+        "-DBDPT_JIT_EMIS=" + std::to_string(c->emis_mask) + "u", "-DBDPT_JIT_GEOM=" + geom,
+        std::string("-DBDPT_WAVES_PER_SIMD=") + (waves ? waves : "6")};
+    const std::string name = "&bdpt_path_kernel_t<" + std::to_string(n) + (streams ? ", true>" : ", false>");
+    std::string key = name;
+    for (const std::string& o : opts) key += " " + o;
+    const auto it = c->jit_fns.find(key);
+    if (it != c->jit_fns.end()) return it->second;
+
+    uint64_t h = 1469598103934665603ull;
+    h = fnv1a(h, kJitMain, sizeof kJitMain);
+    for (int i = 0; i < kJitNumHeaders; i++) h = fnv1a(h, kJitHeaders[i], strlen(kJitHeaders[i]));
+    h = fnv1a(h, key.data(), key.size());
+    char hex[40];
+    snprintf(hex, sizeof hex, "%016llx", (unsigned long long)h);
+    const std::string dir = jit_cache_dir(), path = dir + "/path_" + hex + ".hsaco";
+    const std::string name_path = path + ".name";
+    std::vector<char> code, lowered;
+    if (!read_file(path, code) || !read_file(name_path, lowered)) {
+        hiprtcProgram prog = nullptr;
+        if (api.create(&prog, kJitMain, kJitMainName, kJitNumHeaders, kJitHeaders, kJitHeaderNames) != HIPRTC_SUCCESS) {
+            snprintf(c->jit_err, sizeof c->jit_err, "hiprtcCreateProgram failed");
+            return nullptr;
+        }
+        api.add_name(prog, name.c_str());
+        std::vector<const char*> o;
+        for (const std::string& x : opts) o.push_back(x.c_str());
+        const hiprtcResult rc = api.compile(prog, (int)o.size(), o.data());
+        const char* low = nullptr;
+        size_t sz = 0;
+        if (rc != HIPRTC_SUCCESS || api.lowered(prog, name.c_str(), &low) != HIPRTC_SUCCESS || !low ||
+            api.code_size(prog, &sz) != HIPRTC_SUCCESS || sz == 0) {
+            size_t ls = 0;
+            std::string log;
+            if (api.log_size(prog, &ls) == HIPRTC_SUCCESS && ls > 1) {
+                log.resize(ls);
+                api.log(prog, &log[0]);
+            }
+            snprintf(c->jit_err, sizeof c->jit_err, "hipRTC compile failed: %.200s", log.c_str());
+            api.destroy(&prog);
+            return nullptr;
+        }
+        code.resize(sz);
+        api.code(prog, code.data());
+        lowered.assign(low, low + strlen(low) + 1);
+        api.destroy(&prog);
+        write_file_atomic(dir, path, code);
+        write_file_atomic(dir, name_path, lowered);
+    }
+    if (lowered.empty() || lowered.back() != '\0') lowered.push_back('\0');
+    hipModule_t mod = nullptr;
+    hipFunction_t fn = nullptr;
+    if (hipModuleLoadData(&mod, code.data()) != hipSuccess ||
+        hipModuleGetFunction(&fn, mod, lowered.data()) != hipSuccess) {
+        if (mod) (void)hipModuleUnload(mod);
+        (void)hipGetLastError();
+        snprintf(c->jit_err, sizeof c->jit_err, "loading the specialised code object failed");
+        return nullptr;
+    }
+    c->jit_mods.push_back(mod);
+    c->jit_fns[key] = fn;
+    c->jit_err[0] = 0;
+    return fn;
 }
 
 // Fold the calls issued before call number `upto` into the accumulators, oldest first (waits
@@ -265,6 +464,7 @@ int bdpt_create(bdpt_ctx** out, const bdpt_sphere* spheres, unsigned n, int W, i
         return (fail(c, BDPT_EINVAL, "bdpt_create: bad size %dx%d or spheres", W, H), bail(BDPT_EINVAL));
     c->W = W; c->H = H; c->device = device;
     c->spheres.assign(spheres, spheres + n);
+    if (const char* e = getenv("BDPT_SPECIALIZE")) c->specialize = atoi(e) != 0;   // default for new contexts
     // loadMTGPU (MersenneTwister_kernel.cu:23-36): 4096 x 16 B records
     FILE* f = fopen(mt_dat_path ? mt_dat_path : "assets/data/MersenneTwister.dat", "rb");
     if (!f) return (fail(c, BDPT_EIO, "initMTGPU(): failed to open %s", mt_dat_path), bail(BDPT_EIO));
@@ -356,6 +556,16 @@ int bdpt_set_streams(bdpt_ctx* c, int streams) {
 }
 
 int bdpt_last_streams(const bdpt_ctx* c) { return c ? c->last_streams : BDPT_EINVAL; }
+
+int bdpt_set_specialize(bdpt_ctx* c, int on) {
+    if (!c) return BDPT_EINVAL;
+    c->specialize = on != 0;
+    return BDPT_OK;
+}
+
+int bdpt_last_specialized(const bdpt_ctx* c) { return c ? (int)c->last_specialized : BDPT_EINVAL; }
+
+const char* bdpt_specialize_status(const bdpt_ctx* c) { return c ? c->jit_err : "null context"; }
 
 int bdpt_set_traversal(bdpt_ctx* c, int mode) {
     if (!c) return BDPT_EINVAL;
@@ -558,10 +768,16 @@ int bdpt_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int npass
         // S per launch: a short last chunk gets no idle stream slices
         a.streams = S < a.npass ? S : a.npass;
         const void* kern = bdpt_path_kernel_table[(a.streams > 1) * 18 + kidx];
+        const hipFunction_t jf = bvh ? nullptr : jit_path_kernel(c, a.streams > 1);
+        c->last_specialized = jf != nullptr;
         void* kargs[] = {&a};
         grid.z = a.streams;
         HIPCHK(c, hipEventRecord(cs.kev[2 * launches], c->stream));
-        HIPCHK(c, hipLaunchKernel(kern, grid, block, kargs, smem, c->stream));
+        if (jf)
+            HIPCHK(c, hipModuleLaunchKernel(jf, grid.x, grid.y, grid.z, block.x, 1, 1, (unsigned)smem,
+                                            c->stream, kargs, nullptr));
+        else
+            HIPCHK(c, hipLaunchKernel(kern, grid, block, kargs, smem, c->stream));
         HIPCHK(c, hipEventRecord(cs.kev[2 * launches + 1], c->stream));
         if (a.streams > 1) {
             grid.z = 1;

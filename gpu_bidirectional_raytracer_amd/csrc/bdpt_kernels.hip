@@ -7,11 +7,23 @@
 // steps of device.cu:565-566,594 kept in fp64, and sinf/cosf evaluated as (float)sincos((double)x).
 // Every float operation below is in the reference's order; reordering any of them changes
 // results (SURVEY.md 7 "Hard parts").
+#ifndef __HIPCC_RTC__                       // hipRTC provides the HIP runtime itself
 #include <hip/hip_runtime.h>
-#include <stdint.h>
 #include <utility>
+#endif
 #include "bdpt_device.h"
 #include "bdpt_math.h"
+
+// Run-time specialised build (bdpt_host.cpp jit_path_kernel, hipRTC): only the path kernel, with
+// the scene's sphere geometry {p, rad^2} (exact hex-float literals) and emitter mask as
+// compile-time constants, so that every coordinate difference p - o the spheres share is formed
+// once per ray and the scalar scene loads disappear.  The float operations are the same, in the
+// same order, so the results equal the precompiled instance's bit for bit.
+#ifdef BDPT_JIT
+struct jit_geom { float x, y, z, w; };
+constexpr jit_geom kJitGeom[BDPT_JIT_N] = BDPT_JIT_GEOM;
+constexpr unsigned kJitEmis = BDPT_JIT_EMIS;
+#endif
 
 namespace {
 
@@ -144,6 +156,7 @@ __device__ __forceinline__ f3 cosine_dir(f3 w, float u_phi, float u_r2, const do
 
 }  // namespace
 
+#ifndef BDPT_JIT
 // =============================================================================================
 // Kernel 1: MT607 table (RandomGPU MersenneTwister_kernel.cu:63-110).  4096 independent twisters,
 // lane-major output d_Rand[tid + k*4096].  The 19-word state lives in VGPRs: the recurrence is
@@ -243,6 +256,8 @@ extern "C" __global__ __launch_bounds__(64) void bdpt_light_kernel(const bdpt_de
     }
     lp[ind] = out;
 }
+
+#endif  // BDPT_JIT
 
 // =============================================================================================
 // Kernel 3: the eye-path integrator (RadiancePathTracingKernel device.cu:544-791), `npass`
@@ -356,6 +371,8 @@ extern "C" int bdpt_debug_stats(unsigned long long* out, int reset) {
 #ifndef BDPT_WAVES_PER_SIMD
 #define BDPT_WAVES_PER_SIMD 5
 #endif
+// (the specialised build is compiled with -DBDPT_WAVES_PER_SIMD=6: folding the scene in frees
+// registers, and 6 waves/SIMD measured +3 % over 5 on cornell)
 // BVH scenes: 5 waves/SIMD too, although the traversal state spills 10 VGPRs at 96 (measured:
 // 4 waves +0 spills is 10-12 % slower, 6 waves spills 27).
 #ifndef BDPT_BVH_WAVES
@@ -435,9 +452,18 @@ __global__ __launch_bounds__(256, N < 0 ? BDPT_BVH_WAVES : BDPT_WAVES_PER_SIMD) 
     __syncthreads();
 
     auto geom = [&](int s) -> float4 {
+#ifdef BDPT_JIT
+        if constexpr (N == BDPT_JIT_N) {                        // the scene, folded in
+            const jit_geom g = kJitGeom[s];
+            return make_float4(g.x, g.y, g.z, g.w);
+        }
+#endif
         if constexpr (N > 0) return ld_const(a.geom, s); else return G[s];
     };
     auto emissive = [&](int s) -> bool {
+#ifdef BDPT_JIT
+        if constexpr (N == BDPT_JIT_N) return (kJitEmis >> s) & 1u;
+#endif
         if constexpr (N > 0) return (a.emis_mask >> s) & 1u;
         else return (__float_as_int(C[s].w) & 256) != 0;
     };
@@ -787,6 +813,7 @@ __global__ __launch_bounds__(256, N < 0 ? BDPT_BVH_WAVES : BDPT_WAVES_PER_SIMD) 
     a.pixels[i] = bdpt_dev_to_rgba(col.x, col.y, col.z, a.gamma_thr);
 }
 
+#ifndef BDPT_JIT
 // host-side launch table: [streams * 18 + k], k = sphere count (0 = generic LDS traversal) or 17 = BVH
 #define BDPT_K(NN, ST) (const void*)&bdpt_path_kernel_t<NN, ST>
 #define BDPT_ROW(ST) BDPT_K(0, ST), BDPT_K(1, ST), BDPT_K(2, ST), BDPT_K(3, ST), BDPT_K(4, ST), \
@@ -841,3 +868,4 @@ extern "C" __global__ __launch_bounds__(256) void bdpt_pixels_kernel(const bdpt_
     const bdpt_dev_vec c = colors[i];
     pixels[i] = bdpt_dev_to_rgba(c.x, c.y, c.z, thr);
 }
+#endif  // BDPT_JIT

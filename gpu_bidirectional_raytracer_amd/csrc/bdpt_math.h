@@ -12,7 +12,9 @@
 #ifndef BDPT_MATH_H
 #define BDPT_MATH_H
 
+#ifndef __HIPCC_RTC__
 #include <math.h>
+#endif
 
 #include "bdpt_sincos_table.h"
 

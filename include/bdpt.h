@@ -83,6 +83,14 @@ int  bdpt_set_shard(bdpt_ctx *ctx, int shard, int nshards, int band_rows);
 int  bdpt_set_streams(bdpt_ctx *ctx, int streams);
 /* S used by the last bdpt_path_passes call. */
 int  bdpt_last_streams(const bdpt_ctx *ctx);
+/* Scene-specialised kernels (no reference counterpart; results are bit-identical): for scenes of
+ * <= 32 spheres (brute-force traversal) the path kernel is compiled at run time (hipRTC, ~1 s, cached on disk) with the
+ * sphere geometry folded in as constants.  1 = on (default), 0 = precompiled kernels only.  If
+ * hipRTC is unavailable or the compile fails, the precompiled kernel runs. */
+int  bdpt_set_specialize(bdpt_ctx *ctx, int on);
+/* 1 if the last bdpt_path_passes call ran a specialised kernel; the reason it did not, if not. */
+int  bdpt_last_specialized(const bdpt_ctx *ctx);
+const char *bdpt_specialize_status(const bdpt_ctx *ctx);
 /* Sphere traversal (no reference counterpart; results are bit-identical either way).  The
  * reference tests every sphere per ray (IntersectDevice device.cu:106-124); for scenes with
  * > 16 spheres of which >= 24 are of ordinary size, bdpt_set_scene also builds a BVH over those

@@ -12,11 +12,12 @@ the GLUT idle loop and key handlers driving the render path, on top of the CPU r
 Buffers follow the documented fixes: AllocateBuffers zeroes the counter
 (smallpt_cpu.c:204) and the colors follow from `counter == 0` assigning; the MT table and
 dev_lp persist across a re-allocation (Appendix A.6) instead of being left uninitialised.
-`rand()` is glibc's, seeded 1 as by default (ctypes on libc.so.6).
+`rand()` is glibc's, seeded 1 as by default: GlibcRand restates glibc's random_r TYPE_3 with
+private state (pinned against libc.so.6's rand() in tests/test_replay_host.py).  Calling
+libc's rand() itself would share the process-global state with every library in the process
+(an in-process compiler draws from it, shifting the sequence under the test).
 """
 from __future__ import annotations
-
-import ctypes
 
 import numpy as np
 
@@ -27,13 +28,49 @@ MAX_ITER = 3          # smallpt_cpu.c: flag cycles 2 -> 3 -> (vlp_index += MAX_V
 MAX_VLP = 1
 
 
+class GlibcRand:
+    """glibc rand()/srand() (stdlib/random_r.c, TYPE_3: x**31 + x**3 + 1, 310 discarded
+    outputs after seeding), with the state owned by this object."""
+
+    def __init__(self, seed: int = 1):
+        self.srand(seed)
+
+    def srand(self, seed: int) -> None:
+        seed = seed & 0xFFFFFFFF or 1
+        r = [seed if seed < 2**31 else seed - 2**32]
+        word = r[0]
+        for _ in range(1, 31):                       # 16807 * word % (2^31 - 1), Schrage's method
+            hi = abs(word) // 127773 * (1 if word >= 0 else -1)       # C division truncates
+            lo = word - hi * 127773
+            word = 16807 * lo - 2836 * hi
+            if word < 0:
+                word += 2147483647
+            r.append(word)
+        self._r = [x & 0xFFFFFFFF for x in r]
+        self._f, self._b = 3, 0
+        for _ in range(310):
+            self.rand()
+
+    def rand(self) -> int:
+        val = (self._r[self._f] + self._r[self._b]) & 0xFFFFFFFF
+        self._r[self._f] = val
+        self._f += 1
+        if self._f >= 31:
+            self._f = 0
+            self._b += 1
+        else:
+            self._b += 1
+            if self._b >= 31:
+                self._b = 0
+        return val >> 1
+
+
 class Session:
     """One reference process: globals of smallpt_cpu.c / display_func.c as attributes."""
 
     def __init__(self, spheres: np.ndarray, orig, target, width: int, height: int,
                  rows: tuple[int, int] | None = None):
-        self._libc = ctypes.CDLL("libc.so.6")
-        self._libc.srand(1)
+        self._rand = GlibcRand(1)
         self.spheres = np.ascontiguousarray(spheres.astype(SPHERE_DTYPE, copy=True))
         self.width, self.height = width, height          # internal (+1 applied by caller)
         self.camera = update_camera(orig, target, width, height)
@@ -59,7 +96,7 @@ class Session:
         self.flag = 2
 
     def UpdateRendering(self):
-        sid = self._libc.rand() % RAND_N
+        sid = self._rand.rand() % RAND_N
         vlp = self.vlp_index % 4096                      # Appendix A.3 wrap
         self.colors, self.counter, self.pixels = path_passes(
             self.spheres, self.rnd, self.camera, self.width, self.height, self.lp,

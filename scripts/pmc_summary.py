@@ -37,7 +37,7 @@ if len(sys.argv) > 4:
            "valu_lane_utilisation": round(g('SQ_THREAD_CYCLES_VALU') / (64 * g('SQ_ACTIVE_INST_VALU')), 4),
            "l2_hit_rate": round(g('TCC_HIT_sum') / (g('TCC_HIT_sum') + g('TCC_MISS_sum')), 4),
            "scene": cfg.get("scene"), "width": cfg.get("width"), "height": cfg.get("height"),
-           "passes_per_launch": cfg.get("passes_per_step"), "pass_streams": cfg.get("pass_streams"),
+           "passes_per_launch": cfg.get("passes_per_step"), "pass_streams": cfg.get("pass_streams"), "specialized": cfg.get("specialized", False),
            "source": "rocprofv3 --pmc SQ_INSTS_VALU / SQ_THREAD_CYCLES_VALU / SQ_ACTIVE_INST_VALU / "
                      "GRBM_GUI_ACTIVE / TCC_HIT_sum / TCC_MISS_sum (separate passes), scripts/pmc_summary.py"}
     json.dump(rec, open(sys.argv[4], "w"), indent=1)

@@ -57,7 +57,7 @@ for f in sorted(glob.glob(os.path.join(root, "pmc*.log"))):
         cfg, roof = d["config"], d.get("roofline") or {}
         break
 rec = {"scene": cfg.get("scene", "cornell"), "width": cfg.get("width", 1921), "height": cfg.get("height", 1081),
-       "passes_per_launch": float(cfg.get("passes_per_step", 16)), "pass_streams": cfg.get("pass_streams"),
+       "passes_per_launch": float(cfg.get("passes_per_step", 16)), "pass_streams": cfg.get("pass_streams"), "specialized": cfg.get("specialized", False),
        "fetch_reported_bytes_per_launch": int(fetch), "write_reported_bytes_per_launch": int(write),
        "fetch_scale": fscale, "write_scale": wscale,
        "hbm_bytes_per_launch": int(fetch * (fscale or 1.0) + write * (wscale or 1.0)),

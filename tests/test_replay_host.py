@@ -85,3 +85,17 @@ def test_save_ppm_matches_oracle(tmp_path):
         assert raw[len(head):] == px[::-1, :, :3].tobytes()
     for t, n in ((0.0, 0), (1.23456, 17), (999.9996, 1024), (12345.678, 8192)):
         assert g.ppm_name(t, n) == ppm_name(t, n)
+
+
+def test_oracle_rand_matches_libc():
+    """oracle.replay.GlibcRand restates glibc rand(): same sequence as libc.so.6 for several
+    seeds (including 0, which glibc maps to 1, and seeds above 2^31)."""
+    import ctypes
+    from oracle.replay import GlibcRand
+    libc = ctypes.CDLL("libc.so.6")
+    for seed in (1, 0, 7, 12345, 2**31 + 5, 2**32 - 1):
+        libc.srand(ctypes.c_uint(seed))
+        want = [libc.rand() for _ in range(2000)]
+        r = GlibcRand(seed)
+        assert [r.rand() for _ in range(2000)] == want, seed
+    libc.srand(1)
