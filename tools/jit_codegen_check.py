@@ -1,0 +1,98 @@
+"""Offline build of a scene-specialised path kernel (the source hipRTC compiles at run time,
+bdpt_host.cpp jit_path_kernel) with hipcc, for inspection: register counts, spills, and a scan
+of the disassembly for scalar-memory stores (none may appear in code this project runs).
+
+    python tools/jit_codegen_check.py [scene.scn] [--waves 6] [--keep DIR]
+
+Prints one JSON line per kernel instance; exit status 1 if a scalar store is found.
+"""
+import argparse
+import json
+import os
+import re
+import subprocess
+import sys
+import tempfile
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+SCALAR_STORES = re.compile(r"\b(s_store_|s_buffer_store|s_scratch_store|s_dcache_wb|s_dcache_discard|s_atomic|s_buffer_atomic)")
+
+
+def hexf(v):
+    import numpy as np
+    return float(np.float32(v)).hex() + "f"
+
+
+def jit_defines(spheres):
+    """The -D options jit_path_kernel passes (same geometry literals: {p, rad*rad} in fp32)."""
+    import numpy as np
+    parts, emis = [], 0
+    for i, s in enumerate(spheres):
+        rr = np.float32(s["rad"]) * np.float32(s["rad"])
+        parts.append("{" + ",".join(hexf(x) for x in (s["p"][0], s["p"][1], s["p"][2], rr)) + "}")
+        if i < 32 and any(float(e) != 0.0 for e in s["e"]):
+            emis |= 1 << i
+    return [f"-DBDPT_JIT_N={len(spheres)}", f"-DBDPT_JIT_EMIS={emis}u", "-DBDPT_JIT_GEOM={" + ",".join(parts) + "}"]
+
+
+def build(scene, waves, workdir):
+    sys.path.insert(0, REPO)
+    import gpu_bidirectional_raytracer_amd as g
+    _, sp = g.read_scene(scene)
+    n = len(sp)
+    src = os.path.join(REPO, "gpu_bidirectional_raytracer_amd", "csrc", "bdpt_kernels.hip")
+    inst = os.path.join(workdir, "jit_inst.hip")
+    with open(inst, "w") as f:
+        f.write(f'#include "{src}"\n')
+        for st in ("true", "false"):
+            f.write(f"template __global__ void bdpt_path_kernel_t<{n}, {st}>(bdpt_path_args);\n")
+    co = os.path.join(workdir, "jit.o")
+    cmd = [os.path.join(ROCM, "bin", "hipcc"), "--offload-arch=gfx950", "-O3", "-std=c++17",
+           "-ffp-contract=off", "-fno-slp-vectorize", "-fno-gpu-flush-denormals-to-zero",
+           "-DBDPT_JIT=1", f"-DBDPT_WAVES_PER_SIMD={waves}", *jit_defines(sp),
+           "--cuda-device-only", "-c", "-o", co, inst]
+    subprocess.check_call(cmd)
+    dev = os.path.join(workdir, "jit_dev.o")
+    llvm = os.path.join(ROCM, "lib", "llvm", "bin")
+    with open(co, "rb") as f:
+        bundled = f.read(24).startswith(b"__CLANG_OFFLOAD_BUNDLE__")
+    if bundled:
+        subprocess.check_call([os.path.join(llvm, "clang-offload-bundler"), "--unbundle", "--type=o",
+                               f"--input={co}", "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={dev}"])
+    else:
+        dev = co
+    asm = subprocess.check_output([os.path.join(llvm, "llvm-objdump"), "-d", dev], text=True)
+    notes = subprocess.check_output([os.path.join(llvm, "llvm-readelf"), "--notes", dev], text=True)
+    return asm, notes
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("scene", nargs="?", default=os.path.join(REPO, "assets", "scenes", "cornell.scn"))
+    ap.add_argument("--waves", type=int, default=6)
+    ap.add_argument("--keep", default=None)
+    args = ap.parse_args()
+    with tempfile.TemporaryDirectory() as tmp:
+        wd = args.keep or tmp
+        os.makedirs(wd, exist_ok=True)
+        asm, notes = build(args.scene, args.waves, wd)
+    bad = [l.strip() for l in asm.splitlines() if SCALAR_STORES.search(l)]
+    kernels, cur = [], None
+    for line in notes.splitlines():
+        m = re.match(r"\s*\.(name|vgpr_count|sgpr_count|vgpr_spill_count|sgpr_spill_count):\s+(\S+)", line)
+        if not m:
+            continue
+        if m.group(1) == "name":
+            cur = {"name": m.group(2)}
+            kernels.append(cur)
+        elif cur is not None:
+            cur[m.group(1)] = int(m.group(2))
+    for k in kernels:
+        print(json.dumps(k))
+    print(json.dumps({"scalar_stores": len(bad), "first": bad[:3]}))
+    return 1 if bad else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
