@@ -24,7 +24,7 @@ if [ -n "${PMC_MIX:-}" ]; then PMC_SETS=(
 for s in $STEPS; do
   case "$s" in
   tests)
-    timeout -k 10 600 python -m pytest tests -m gpu -q -rA > gpurun_out/pytest_gpu.log 2>&1
+    timeout -k 10 900 python -u -m pytest tests -m gpu -v -rA --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
     rc=$?; tail -30 gpurun_out/pytest_gpu.log; ok_or_stop $rc tests ;;
   smoke)
     timeout -k 10 300 python -c "import __graft_entry__ as e; e.smoke()" > gpurun_out/smoke.log 2>&1

@@ -1,6 +1,7 @@
 import os
 import subprocess
 import sys
+import tempfile
 
 import pytest
 
@@ -12,6 +13,9 @@ for _p in (REPO, os.path.join(REPO, "tests", "golden")):
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP kernels)")
+    # scene-specialised kernels compile into a cache private to this test session, so no code
+    # object from an earlier build or toolchain can stand in for the current sources
+    os.environ.setdefault("BDPT_JIT_CACHE", tempfile.mkdtemp(prefix="bdpt-jit-test-"))
     # build the in-tree artefacts once if they are missing (cheap no-op otherwise)
     need = [os.path.join(REPO, "gpu_bidirectional_raytracer_amd", "libbdpt.so"),
             os.path.join(REPO, "oracle", "liboracle.so")]

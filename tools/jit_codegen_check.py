@@ -1,10 +1,17 @@
 """Offline build of a scene-specialised path kernel (the source hipRTC compiles at run time,
-bdpt_host.cpp jit_path_kernel) with hipcc, for inspection: register counts, spills, and a scan
-of the disassembly for scalar-memory stores (none may appear in code this project runs).
+bdpt_host.cpp jit_path_kernel) with hipcc, for inspection: register counts, spills, and a check
+that the code writes nothing through the scalar data cache.
 
     python tools/jit_codegen_check.py [scene.scn] [--waves 6] [--keep DIR]
 
-Prints one JSON line per kernel instance; exit status 1 if a scalar store is found.
+Prints one JSON line per kernel instance and one summary line; exit status 1 if an instance
+spills or a scalar-memory write is found.
+
+The scalar-write check decodes the machine words, not the disassembler's text: every
+instruction in the SMEM encoding (first dword bits [31:26] = 0b110000 on gfx9-family targets,
+opcode in bits [25:18]) is classified by opcode number.  Loads (0-12), cache invalidates (32, 34)
+and the time / probe reads (36-39) are allowed; every other SMEM opcode (stores 16-26,
+write-backs 33 and 35, discards 40-41, scalar atomics >= 64) is reported.
 """
 import argparse
 import json
@@ -16,7 +23,8 @@ import tempfile
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
-SCALAR_STORES = re.compile(r"\b(s_store_|s_buffer_store|s_scratch_store|s_dcache_wb|s_dcache_discard|s_atomic|s_buffer_atomic)")
+SMEM_ALLOWED = set(range(0, 13)) | {32, 34, 36, 37, 38, 39}
+ENC_WORD = re.compile(r"//\s*[0-9A-Fa-f]+:\s+([0-9A-Fa-f]{8})")
 
 
 def hexf(v):
@@ -36,7 +44,20 @@ def jit_defines(spheres):
     return [f"-DBDPT_JIT_N={len(spheres)}", f"-DBDPT_JIT_EMIS={emis}u", "-DBDPT_JIT_GEOM={" + ",".join(parts) + "}"]
 
 
-def build(scene, waves, workdir):
+def scalar_writes(asm):
+    """Instructions of the SMEM encoding whose opcode is not a read (see module docstring)."""
+    bad = []
+    for line in asm.splitlines():
+        m = ENC_WORD.search(line)
+        if not m:
+            continue
+        w = int(m.group(1), 16)
+        if (w >> 26) == 0b110000 and ((w >> 18) & 0xFF) not in SMEM_ALLOWED:
+            bad.append(line.strip())
+    return bad
+
+
+def build(scene, waves, workdir, extra=()):
     sys.path.insert(0, REPO)
     import gpu_bidirectional_raytracer_amd as g
     _, sp = g.read_scene(scene)
@@ -51,7 +72,7 @@ def build(scene, waves, workdir):
     cmd = [os.path.join(ROCM, "bin", "hipcc"), "--offload-arch=gfx950", "-O3", "-std=c++17",
            "-ffp-contract=off", "-fno-slp-vectorize", "-fno-gpu-flush-denormals-to-zero",
            "-DBDPT_JIT=1", f"-DBDPT_WAVES_PER_SIMD={waves}", *jit_defines(sp),
-           "--cuda-device-only", "-c", "-o", co, inst]
+           *extra, "--cuda-device-only", "-c", "-o", co, inst]
     subprocess.check_call(cmd)
     dev = os.path.join(workdir, "jit_dev.o")
     llvm = os.path.join(ROCM, "lib", "llvm", "bin")
@@ -72,12 +93,14 @@ def main():
     ap.add_argument("scene", nargs="?", default=os.path.join(REPO, "assets", "scenes", "cornell.scn"))
     ap.add_argument("--waves", type=int, default=6)
     ap.add_argument("--keep", default=None)
+    ap.add_argument("--extra", action="append", default=[], help="extra compiler option (experiments)")
     args = ap.parse_args()
     with tempfile.TemporaryDirectory() as tmp:
         wd = args.keep or tmp
         os.makedirs(wd, exist_ok=True)
-        asm, notes = build(args.scene, args.waves, wd)
-    bad = [l.strip() for l in asm.splitlines() if SCALAR_STORES.search(l)]
+        asm, notes = build(args.scene, args.waves, wd, args.extra)
+    bad = scalar_writes(asm)
+    smem = sum(1 for l in asm.splitlines() if (m := ENC_WORD.search(l)) and int(m.group(1), 16) >> 26 == 0b110000)
     kernels, cur = [], None
     for line in notes.splitlines():
         m = re.match(r"\s*\.(name|vgpr_count|sgpr_count|vgpr_spill_count|sgpr_spill_count):\s+(\S+)", line)
@@ -90,8 +113,9 @@ def main():
             cur[m.group(1)] = int(m.group(2))
     for k in kernels:
         print(json.dumps(k))
-    print(json.dumps({"scalar_stores": len(bad), "first": bad[:3]}))
-    return 1 if bad else 0
+    print(json.dumps({"smem_instructions": smem, "scalar_writes": len(bad), "first": bad[:3]}))
+    spills = any(k.get("vgpr_spill_count", 0) for k in kernels)
+    return 1 if bad or spills else 0
 
 
 if __name__ == "__main__":
