@@ -104,6 +104,7 @@ struct bdpt_ctx {
     std::map<std::string, hipFunction_t> jit_fns;
     std::vector<hipModule_t> jit_mods;
     char jit_err[256] = {0};            // why the last specialisation fell back (diagnostics)
+    int jit_waves = 0;                  // waves/SIMD bound of the last specialised build
     char err[512] = {0};
 };
 
@@ -240,9 +241,12 @@ static void release(bdpt_ctx* c) {
 // 27) and the scalar scene loads go away: +7 % on cornell.  The float operations are the same in
 // the same order, so results are bit-identical to the precompiled kernels
 // (tests/test_gpu_specialize.py).  hipRTC is opened with dlopen; when it is missing or a compile
-// fails, the precompiled instance runs (bdpt_last_specialized() says which one did).  Code objects
-// are cached per context and on disk ($BDPT_JIT_CACHE, else $HOME/.cache/bdpt-jit, else /tmp),
-// keyed by a hash of the sources and options; a compile takes ~1 s.
+// fails, the precompiled instance runs (bdpt_last_specialized() says which one did).  A build that
+// needs scratch (register spills) at 6 waves/SIMD is rebuilt at 5.  Code objects are cached per
+// context and on disk ($BDPT_JIT_CACHE, else $HOME/.cache/bdpt-jit), keyed by a hash of the
+// sources, the options, the hipRTC version and the device's gfx arch; the cache directory must be
+// owned by the user and closed to others (created 0700), else nothing is read from or written to
+// disk.  A compile takes ~1 s.
 #include "bdpt_jit_src.h"
 
 namespace {
@@ -257,6 +261,7 @@ struct rtc_api {
     decltype(&hiprtcGetProgramLogSize) log_size = nullptr;
     decltype(&hiprtcGetProgramLog) log = nullptr;
     decltype(&hiprtcDestroyProgram) destroy = nullptr;
+    int major = 0, minor = 0;                    // hiprtcVersion (part of the cache key)
 };
 
 const rtc_api& rtc() {
@@ -279,8 +284,10 @@ const rtc_api& rtc() {
         BDPT_RTC_SYM(log, "hiprtcGetProgramLog");
         BDPT_RTC_SYM(destroy, "hiprtcDestroyProgram");
 #undef BDPT_RTC_SYM
+        auto version = (decltype(&hiprtcVersion))dlsym(h, "hiprtcVersion");
         r.ok = r.create && r.add_name && r.compile && r.lowered && r.code_size && r.code &&
-               r.log_size && r.log && r.destroy;
+               r.log_size && r.log && r.destroy && version &&
+               version(&r.major, &r.minor) == HIPRTC_SUCCESS;
         return r;
     }();
     return api;
@@ -298,80 +305,81 @@ std::string hexf(float v) {                     // exact float literal
     return b;
 }
 
+// The on-disk cache directory, created 0700 if missing; "" (no disk cache) unless it is a
+// directory owned by this user that neither group nor others can write.
 std::string jit_cache_dir() {
-    if (const char* d = getenv("BDPT_JIT_CACHE")) return d;
-    if (const char* home = getenv("HOME")) return std::string(home) + "/.cache/bdpt-jit";
-    return "/tmp/bdpt-jit-" + std::to_string((long)getuid());
+    std::string dir;
+    if (const char* d = getenv("BDPT_JIT_CACHE")) dir = d;
+    else if (const char* home = getenv("HOME")) dir = std::string(home) + "/.cache/bdpt-jit";
+    else return "";
+    std::string d;                                           // mkdir -p, 0700
+    for (size_t i = 0; i <= dir.size(); i++) {
+        if ((i == dir.size() || dir[i] == '/') && !d.empty()) mkdir(d.c_str(), 0700);
+        if (i < dir.size()) d += dir[i];
+    }
+    struct stat st;
+    if (stat(dir.c_str(), &st) != 0 || !S_ISDIR(st.st_mode) || st.st_uid != getuid() ||
+        (st.st_mode & (S_IWGRP | S_IWOTH)))
+        return "";
+    return dir;
 }
 
 bool read_file(const std::string& path, std::vector<char>& out) {
     FILE* f = fopen(path.c_str(), "rb");
     if (!f) return false;
-    fseek(f, 0, SEEK_END);
-    const long n = ftell(f);
-    fseek(f, 0, SEEK_SET);
-    out.resize(n > 0 ? (size_t)n : 0);
-    const bool ok = n > 0 && fread(out.data(), 1, (size_t)n, f) == (size_t)n;
+    struct stat st;
+    if (fstat(fileno(f), &st) != 0 || st.st_uid != getuid() || !S_ISREG(st.st_mode)) {
+        fclose(f);
+        return false;
+    }
+    out.resize(st.st_size > 0 ? (size_t)st.st_size : 0);
+    const bool ok = st.st_size > 0 && fread(out.data(), 1, out.size(), f) == out.size();
     fclose(f);
     return ok;
 }
 
-void write_file_atomic(const std::string& dir, const std::string& path, const std::vector<char>& data) {
-    std::string d;                                           // mkdir -p
-    for (size_t i = 0; i <= dir.size(); i++) {
-        if (i == dir.size() || dir[i] == '/') {
-            if (!d.empty()) mkdir(d.c_str(), 0755);
-        }
-        if (i < dir.size()) d += dir[i];
-    }
+// Write to a private temporary file and rename it into place only if every byte reached it.
+void write_file_atomic(const std::string& path, const std::vector<char>& data) {
     const std::string tmp = path + ".tmp." + std::to_string((long)getpid());
     FILE* f = fopen(tmp.c_str(), "wb");
     if (!f) return;
-    const bool ok = fwrite(data.data(), 1, data.size(), f) == data.size();
-    fclose(f);
-    if (ok) rename(tmp.c_str(), path.c_str()); else unlink(tmp.c_str());
+    bool ok = fwrite(data.data(), 1, data.size(), f) == data.size();
+    ok = (fflush(f) == 0) && ok;
+    ok = (fclose(f) == 0) && ok;
+    if (ok) ok = rename(tmp.c_str(), path.c_str()) == 0;
+    if (!ok) unlink(tmp.c_str());
 }
 }  // namespace
 
-// The specialised kernel for the context's scene and pass-stream mode, compiled on first use;
-// nullptr = use the precompiled instance (reason in c->jit_err).
-static hipFunction_t jit_path_kernel(bdpt_ctx* c, bool streams) {
-    const unsigned n = (unsigned)c->spheres.size();
-    if (!c->specialize || n < 1 || n > 32) return nullptr;          // kJitEmis is 32 bits
+// Compile (or fetch from the disk cache) and load one specialised build; nullptr on failure
+// (reason in c->jit_err).
+static hipFunction_t jit_build(bdpt_ctx* c, const std::string& name, const std::vector<std::string>& opts) {
     const rtc_api& api = rtc();
-    if (!api.ok) {
-        snprintf(c->jit_err, sizeof c->jit_err, "hipRTC not found");
-        return nullptr;
-    }
-    std::string geom = "{";
-    for (unsigned i = 0; i < n; i++) {
-        const bdpt_sphere& sp = c->spheres[i];
-        const float rr = sp.rad * sp.rad;                    // as upload_scene forms it
-        geom += (i ? ",{" : "{") + hexf(sp.p.x) + "," + hexf(sp.p.y) + "," + hexf(sp.p.z) + "," + hexf(rr) + "}";
-    }
-    geom += "}";
-    const char* waves = getenv("BDPT_JIT_WAVES");
-    std::vector<std::string> opts = {
-        "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize",
-        "-fno-gpu-flush-denormals-to-zero", "-DBDPT_JIT=1", "-DBDPT_JIT_N=" + std::to_string(n),
-        "-DBDPT_JIT_EMIS=" + std::to_string(c->emis_mask) + "u", "-DBDPT_JIT_GEOM=" + geom,
-        std::string("-DBDPT_WAVES_PER_SIMD=") + (waves ? waves : "6")};
-    const std::string name = "&bdpt_path_kernel_t<" + std::to_string(n) + (streams ? ", true>" : ", false>");
     std::string key = name;
     for (const std::string& o : opts) key += " " + o;
     const auto it = c->jit_fns.find(key);
     if (it != c->jit_fns.end()) return it->second;
 
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, c->device) != hipSuccess) {
+        (void)hipGetLastError();
+        snprintf(c->jit_err, sizeof c->jit_err, "hipGetDeviceProperties failed");
+        return nullptr;
+    }
     uint64_t h = 1469598103934665603ull;
     h = fnv1a(h, kJitMain, sizeof kJitMain);
     for (int i = 0; i < kJitNumHeaders; i++) h = fnv1a(h, kJitHeaders[i], strlen(kJitHeaders[i]));
     h = fnv1a(h, key.data(), key.size());
+    const int ver[2] = {api.major, api.minor};
+    h = fnv1a(h, ver, sizeof ver);
+    h = fnv1a(h, prop.gcnArchName, strnlen(prop.gcnArchName, sizeof prop.gcnArchName));
     char hex[40];
     snprintf(hex, sizeof hex, "%016llx", (unsigned long long)h);
-    const std::string dir = jit_cache_dir(), path = dir + "/path_" + hex + ".hsaco";
+    const std::string dir = jit_cache_dir();
+    const std::string path = dir.empty() ? "" : dir + "/path_" + hex + ".hsaco";
     const std::string name_path = path + ".name";
     std::vector<char> code, lowered;
-    if (!read_file(path, code) || !read_file(name_path, lowered)) {
+    if (path.empty() || !read_file(path, code) || !read_file(name_path, lowered)) {
         hiprtcProgram prog = nullptr;
         if (api.create(&prog, kJitMain, kJitMainName, kJitNumHeaders, kJitHeaders, kJitHeaderNames) != HIPRTC_SUCCESS) {
             snprintf(c->jit_err, sizeof c->jit_err, "hiprtcCreateProgram failed");
@@ -399,8 +407,10 @@ static hipFunction_t jit_path_kernel(bdpt_ctx* c, bool streams) {
         api.code(prog, code.data());
         lowered.assign(low, low + strlen(low) + 1);
         api.destroy(&prog);
-        write_file_atomic(dir, path, code);
-        write_file_atomic(dir, name_path, lowered);
+        if (!path.empty()) {
+            write_file_atomic(path, code);
+            write_file_atomic(name_path, lowered);
+        }
     }
     if (lowered.empty() || lowered.back() != '\0') lowered.push_back('\0');
     hipModule_t mod = nullptr;
@@ -414,8 +424,47 @@ static hipFunction_t jit_path_kernel(bdpt_ctx* c, bool streams) {
     }
     c->jit_mods.push_back(mod);
     c->jit_fns[key] = fn;
-    c->jit_err[0] = 0;
     return fn;
+}
+
+// The specialised kernel for the context's scene and pass-stream mode, compiled on first use;
+// nullptr = use the precompiled instance (reason in c->jit_err).
+static hipFunction_t jit_path_kernel(bdpt_ctx* c, bool streams) {
+    const unsigned n = (unsigned)c->spheres.size();
+    if (!c->specialize || n < 1 || n > 32) return nullptr;          // kJitEmis is 32 bits
+    if (!rtc().ok) {
+        snprintf(c->jit_err, sizeof c->jit_err, "hipRTC not found");
+        return nullptr;
+    }
+    std::string geom = "{";
+    for (unsigned i = 0; i < n; i++) {
+        const bdpt_sphere& sp = c->spheres[i];
+        const float rr = sp.rad * sp.rad;                    // as upload_scene forms it
+        geom += (i ? ",{" : "{") + hexf(sp.p.x) + "," + hexf(sp.p.y) + "," + hexf(sp.p.z) + "," + hexf(rr) + "}";
+    }
+    geom += "}";
+    const char* wenv = getenv("BDPT_JIT_WAVES");
+    int waves = wenv ? atoi(wenv) : 6;
+    const std::string name = "&bdpt_path_kernel_t<" + std::to_string(n) + (streams ? ", true>" : ", false>");
+    for (;; waves--) {
+        const std::vector<std::string> opts = {
+            "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize",
+            "-fno-gpu-flush-denormals-to-zero", "-DBDPT_JIT=1", "-DBDPT_JIT_N=" + std::to_string(n),
+            "-DBDPT_JIT_EMIS=" + std::to_string(c->emis_mask) + "u", "-DBDPT_JIT_GEOM=" + geom,
+            "-DBDPT_WAVES_PER_SIMD=" + std::to_string(waves)};
+        hipFunction_t fn = jit_build(c, name, opts);
+        if (!fn) return nullptr;
+        int scratch = 0;
+        if (hipFuncGetAttribute(&scratch, HIP_FUNC_ATTRIBUTE_LOCAL_SIZE_BYTES, fn) != hipSuccess) {
+            (void)hipGetLastError();
+            scratch = 0;
+        }
+        if (scratch == 0 || waves <= 5) {                    // spill-free, or the 5-wave floor
+            c->jit_err[0] = 0;
+            c->jit_waves = waves;
+            return fn;
+        }
+    }
 }
 
 // Fold the calls issued before call number `upto` into the accumulators, oldest first (waits
@@ -460,7 +509,7 @@ int bdpt_create(bdpt_ctx** out, const bdpt_sphere* spheres, unsigned n, int W, i
         delete c;
         return code;
     };
-    if (W <= 0 || H <= 0 || (long)W * (long)H > (1L << 30) || (n > 0 && !spheres))
+    if (W <= 0 || H <= 0 || W > 65535 || H > 65535 || (long)W * (long)H > (1L << 30) || (n > 0 && !spheres))
         return (fail(c, BDPT_EINVAL, "bdpt_create: bad size %dx%d or spheres", W, H), bail(BDPT_EINVAL));
     c->W = W; c->H = H; c->device = device;
     c->spheres.assign(spheres, spheres + n);
@@ -746,6 +795,16 @@ int bdpt_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int npass
         HIPCHK(c, hipEventCreate(&e));
         cs.kev.push_back(e);
     }
+    // resolve the specialised kernels (a compile on first use) before the timed region starts
+    hipFunction_t jf_streams = nullptr, jf_fused = nullptr;
+    if (!bvh && grid_rows > 0) {
+        for (int p0 = 0; p0 < npass; p0 += chunk) {
+            const int np = npass - p0 < chunk ? npass - p0 : chunk;
+            const bool st = (S < np ? S : np) > 1;
+            if (st && !jf_streams) jf_streams = jit_path_kernel(c, true);
+            if (!st && !jf_fused) jf_fused = jit_path_kernel(c, false);
+        }
+    }
     HIPCHK(c, hipEventRecord(cs.ev0, c->stream));
     int launches = 0;
     for (int p0 = 0; grid_rows > 0 && p0 < npass; p0 += chunk, launches++) {
@@ -768,7 +827,7 @@ int bdpt_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int npass
         // S per launch: a short last chunk gets no idle stream slices
         a.streams = S < a.npass ? S : a.npass;
         const void* kern = bdpt_path_kernel_table[(a.streams > 1) * 18 + kidx];
-        const hipFunction_t jf = bvh ? nullptr : jit_path_kernel(c, a.streams > 1);
+        const hipFunction_t jf = a.streams > 1 ? jf_streams : jf_fused;
         c->last_specialized = jf != nullptr;
         void* kargs[] = {&a};
         grid.z = a.streams;

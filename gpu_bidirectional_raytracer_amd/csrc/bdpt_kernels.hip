@@ -378,8 +378,14 @@ extern "C" int bdpt_debug_stats(unsigned long long* out, int reset) {
 #ifndef BDPT_BVH_WAVES
 #define BDPT_BVH_WAVES 5
 #endif
+// The fused S = 1 kernel keeps the running mean and the counter in registers too (4 more live
+// values): at 6 waves/SIMD it would spill, so it is bounded at 5 (it is the non-default mode).
+#ifndef BDPT_FUSED_WAVES
+#define BDPT_FUSED_WAVES (BDPT_WAVES_PER_SIMD < 5 ? BDPT_WAVES_PER_SIMD : 5)
+#endif
 template <int N, bool STREAMS>
-__global__ __launch_bounds__(256, N < 0 ? BDPT_BVH_WAVES : BDPT_WAVES_PER_SIMD) void bdpt_path_kernel_t(bdpt_path_args a) {
+__global__ __launch_bounds__(256, N < 0 ? BDPT_BVH_WAVES : (STREAMS ? BDPT_WAVES_PER_SIMD : BDPT_FUSED_WAVES))
+void bdpt_path_kernel_t(bdpt_path_args a) {
     extern __shared__ float4 smem[];
     constexpr bool kBVH = N < 0;      // large scene: walls brute force + BVH (bdpt_bvh.cpp)
     const int n = N > 0 ? N : (int)a.n;
@@ -488,6 +494,11 @@ __global__ __launch_bounds__(256, N < 0 ? BDPT_BVH_WAVES : BDPT_WAVES_PER_SIMD) 
 
     const int i = active ? y * a.W + x : 0;
     const unsigned ibase = 26u + (unsigned)(i * 25);
+    // The pixel coordinates live in one packed register (W, H < 2^16, bdpt_create) and are
+    // unpacked where they are used, behind an empty asm the compiler cannot look through: left
+    // to itself it hoists (float)x, (float)y and the 64-bit pass-stream store address out of the
+    // path loop and then spills them at the 80-VGPR (6 waves/SIMD) bound.
+    const unsigned xy = ((unsigned)y << 16) | (unsigned)x;
     const float* __restrict__ rnd = a.rnd;
     constexpr unsigned M5 = kRandN - 5u;
 
@@ -502,8 +513,8 @@ __global__ __launch_bounds__(256, N < 0 ? BDPT_BVH_WAVES : BDPT_WAVES_PER_SIMD) 
     }
 
     int p = s0;
-    unsigned depth = 0, sid = SID[p < a.npass ? p : 0];
-    unsigned j = (ibase + sid) % M5;
+    unsigned depth = 0;
+    unsigned j = (ibase + SID[p < a.npass ? p : 0]) % M5;
     float q0 = rnd[j], q1 = rnd[j + 1], q2 = rnd[j + 2], q3 = rnd[j + 3], q4 = rnd[j + 4];
     f3 ro = mk(0.f, 0.f, 0.f), rd = ro, thr = ro, rad = ro, nl = ro;
     bool specular = true, fresh = true;
@@ -522,6 +533,9 @@ __global__ __launch_bounds__(256, N < 0 ? BDPT_BVH_WAVES : BDPT_WAVES_PER_SIMD) 
         bool done = false, diff = false;
         if (alive) {
             if (fresh) {                  // camera ray (:562-600); d_Rand[kk] == q0 (kk == j)
+                unsigned xyv = xy;
+                asm volatile("" : "+v"(xyv));
+                const int x = (int)(xyv & 0xffffu), y = (int)(xyv >> 16);
                 const float4 c0 = K[0], c1 = K[1], c2 = K[2], c3 = K[3], k4 = K[4];
                 // device.cu:565-566: ((float)x*iw - iw*W/2.) + d_Rand[kk]*iw in fp64, then fp32
                 const float kx = (float)(((double)((float)x * k4.x) - a.half_w) + (double)(q0 * k4.x));
@@ -790,16 +804,23 @@ __global__ __launch_bounds__(256, N < 0 ? BDPT_BVH_WAVES : BDPT_WAVES_PER_SIMD) 
                 } else {
                     bdpt_dev_vec r;
                     r.x = rad.x; r.y = rad.y; r.z = rad.z;
-                    a.rbuf[(size_t)p * a.nloc + (size_t)(i - yoff * a.W)] = r;
+                    unsigned xyv = xy;
+                    asm volatile("" : "+v"(xyv));
+                    const int li = ((int)(xyv >> 16) - yoff) * a.W + (int)(xyv & 0xffffu);
+                    a.rbuf[(size_t)p * a.nloc + (size_t)li] = r;
                 }
                 p += S;
                 fresh = true;
                 depth = 0;
                 alive = p < a.npass && cnt0 + (unsigned)p < BDPT_DEV_COUNTER_CAP;
-                if (alive) sid = SID[p];
             }
             if (alive) {                  // prefetch the next segment's random numbers (:619)
-                j = (ibase + depth * 5u + sid) % M5;
+                // 26 + 25 i and the pass's sid are rebuilt here rather than kept live across the
+                // loop (one LDS read and four integer ops per segment, against a spill)
+                unsigned xyv = xy;
+                asm volatile("" : "+v"(xyv));
+                const unsigned li = (xyv >> 16) * (unsigned)a.W + (xyv & 0xffffu);
+                j = (26u + li * 25u + depth * 5u + SID[p]) % M5;
                 q0 = rnd[j]; q1 = rnd[j + 1]; q2 = rnd[j + 2]; q3 = rnd[j + 3]; q4 = rnd[j + 4];
             }
         }

@@ -48,6 +48,11 @@ def test_specialised_build_offline(scene):
     kernels = [k for k in recs if "name" in k]
     assert len(kernels) == 2, r.stdout + r.stderr
     assert recs[-1]["smem_instructions"] > 0 and recs[-1]["scalar_writes"] == 0, recs[-1]
-    for k in kernels:
-        assert k["vgpr_count"] <= 80 and k["vgpr_spill_count"] == 0, k
+    for k in kernels:                    # the build the host keeps (6 waves/SIMD, else 5)
+        assert k["vgpr_spill_count"] == 0, k
+        assert k["vgpr_count"] <= 512 // 8 // k["waves"] * 8, k
+    # the default (pass-stream) kernel of the benchmark scenes keeps 6 waves/SIMD
+    streams = [k for k in kernels if "Lb1E" in k["name"]]
+    if scene in ("cornell", "cornell_glass", "caustic"):
+        assert streams[0]["waves"] == 6, streams
     assert r.returncode == 0, r.stdout + r.stderr

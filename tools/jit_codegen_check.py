@@ -88,19 +88,7 @@ def build(scene, waves, workdir, extra=()):
     return asm, notes
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("scene", nargs="?", default=os.path.join(REPO, "assets", "scenes", "cornell.scn"))
-    ap.add_argument("--waves", type=int, default=6)
-    ap.add_argument("--keep", default=None)
-    ap.add_argument("--extra", action="append", default=[], help="extra compiler option (experiments)")
-    args = ap.parse_args()
-    with tempfile.TemporaryDirectory() as tmp:
-        wd = args.keep or tmp
-        os.makedirs(wd, exist_ok=True)
-        asm, notes = build(args.scene, args.waves, wd, args.extra)
-    bad = scalar_writes(asm)
-    smem = sum(1 for l in asm.splitlines() if (m := ENC_WORD.search(l)) and int(m.group(1), 16) >> 26 == 0b110000)
+def kernel_notes(notes):
     kernels, cur = [], None
     for line in notes.splitlines():
         m = re.match(r"\s*\.(name|vgpr_count|sgpr_count|vgpr_spill_count|sgpr_spill_count):\s+(\S+)", line)
@@ -111,10 +99,38 @@ def main():
             kernels.append(cur)
         elif cur is not None:
             cur[m.group(1)] = int(m.group(2))
-    for k in kernels:
+    return kernels
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("scene", nargs="?", default=os.path.join(REPO, "assets", "scenes", "cornell.scn"))
+    ap.add_argument("--waves", type=int, default=6)
+    ap.add_argument("--keep", default=None)
+    ap.add_argument("--extra", action="append", default=[], help="extra compiler option (experiments)")
+    args = ap.parse_args()
+    # the host's policy (bdpt_host.cpp jit_path_kernel): a build that spills is rebuilt with one
+    # wave per SIMD fewer, down to 5
+    final, bad, smem = {}, [], 0
+    for waves in range(args.waves, 4, -1):
+        with tempfile.TemporaryDirectory() as tmp:
+            wd = args.keep or tmp
+            os.makedirs(wd, exist_ok=True)
+            asm, notes = build(args.scene, waves, wd, args.extra)
+        bad += scalar_writes(asm)
+        smem += sum(1 for l in asm.splitlines()
+                    if (m := ENC_WORD.search(l)) and int(m.group(1), 16) >> 26 == 0b110000)
+        for k in kernel_notes(notes):
+            if k["name"] not in final or final[k["name"]]["vgpr_spill_count"]:
+                # launch bound of the instance: the fused S = 1 kernel is capped at 5
+                # (bdpt_kernels.hip BDPT_FUSED_WAVES)
+                final[k["name"]] = dict(k, waves=min(waves, 5) if "Lb0E" in k["name"] else waves)
+        if not any(k["vgpr_spill_count"] for k in final.values()):
+            break
+    for k in final.values():
         print(json.dumps(k))
     print(json.dumps({"smem_instructions": smem, "scalar_writes": len(bad), "first": bad[:3]}))
-    spills = any(k.get("vgpr_spill_count", 0) for k in kernels)
+    spills = any(k.get("vgpr_spill_count", 0) for k in final.values())
     return 1 if bad or spills else 0
 
 
