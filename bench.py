@@ -1,18 +1,26 @@
 #!/usr/bin/env python3
-"""bench.py -- path-pass throughput (Msamples/s) of the MI355X path tracer at 1080p cornell.scn.
+"""bench.py -- path-pass throughput (Msamples/s) of the MI355X path tracer.
 
-One "step" = `--passes` x N fused path passes (RadiancePathTracingKernel, device.cu:544) over this
-rank's pixel bands of the 1921x1081 frame (CLI 1920x1080 + the reference's +1).  Weak scaling:
-each rank owns 1/N of the pixels (16-row bands interleaved over ranks) and renders N x passes per
-step, so the per-GPU work is constant and the job renders N x the spp of the same frame.  The
-timed region ends with the RCCL (torch.distributed "nccl") sum-reduce of the radiance frame to
-rank 0, which assembles the image (pixels outside a rank's bands are zero, so the sum is exact).
+One "step" = one batch of fused path passes (RadiancePathTracingKernel, device.cu:544) over this
+rank's pixels.  Workloads (`--workload`, BASELINE.json configs):
 
-Prints ONE JSON line on rank 0 (see DESIGN.md "Measurement" for every field).
+  cornell1080 (default; the metric's config, configs[1] at 1080p): cornell.scn 1921x1081 internal
+      (CLI 1920x1080 + the reference's +1).  Weak scaling: each rank owns 1/N of the pixels
+      (8-row bands interleaved over ranks) and renders N x `--passes` passes per step, so the
+      per-GPU work is constant and the job renders N x the spp of the same frame.
+  caustic8 (configs[3]): caustic.scn 1921x1081, 8-row interleaved bands over N ranks, `--passes`
+      passes of the whole frame per step.  Strong scaling (the frame and spp are fixed).
+  weak64 (configs[4]): the 64-sphere synthetic scene at 4097x4097, cut into 8 bands of 512 rows;
+      rank r renders band r (1 GPU: one 4097x512 band, 8 GPUs: the full frame).  Weak scaling.
+
+With N > 1 the timed region ends with the RCCL (torch.distributed "nccl") sum-reduce of the
+radiance frame to rank 0, which assembles the image (pixels outside a rank's bands are zero, so
+the sum is exact).  Prints ONE JSON line on rank 0 (see DESIGN.md "Measurement" for the fields).
 """
 import argparse
 import json
 import os
+import socket
 import sys
 import time
 
@@ -21,8 +29,17 @@ sys.path.insert(0, REPO)
 
 METRIC = "Msamples/sec (rays·bounces/s) at 1080p cornell.scn, 1/2/4/8 GPU"
 
-# Per-sample work of the workload, measured once by the CPU restatement over the full 1921x1081
-# cornell frame (tests/test_work_model.py keeps these honest; DESIGN.md "Roofline").
+WORKLOADS = {
+    "cornell1080": dict(scene="cornell", width=1920, height=1080, passes=32, band_rows=8, fixed_bands=0,
+                        scaling="weak", config="configs[1] scene at 1080p (the metric's config)"),
+    "caustic8": dict(scene="caustic", width=1920, height=1080, passes=128, band_rows=8, fixed_bands=0,
+                     scaling="strong", config="configs[3]: caustic.scn 1920x1080, pixel bands over N GPUs"),
+    "weak64": dict(scene="synthetic64", width=4096, height=4096, passes=128, band_rows=512, fixed_bands=8,
+                   scaling="weak", config="configs[4]: 64-sphere synthetic 4096x4096, one 4097x512 band per GPU"),
+}
+
+# Per-sample work of each scene, measured once by the CPU restatement over the full 1921x1081
+# frame (tests/test_work_model.py keeps these honest; DESIGN.md "Roofline").
 WORK = {
     "cornell": {"sphere_tests": 129.4711, "segments": 6.8441, "diffuse": 6.1386, "refr": 0.4528, "rng_reads": 27.0071},
     "cornell_glass": {"sphere_tests": 92.9047, "segments": 6.8374, "diffuse": 4.2323, "refr": 1.02, "rng_reads": 19.9494},
@@ -41,8 +58,11 @@ WORK = {
 FLOP = {"sphere_tests": 18, "segments": 28, "diffuse": 153, "refr": 40, "per_sample": 59}
 ACCUM_BYTES_PER_PIXEL = 36       # colors 12R+12W, counter 4R+4W, pixels 4W per launch
 HBM_PEAK_GBS = 8000.0            # MI355X HBM3E spec (MI355X_MICROARCH.md)
-FP32_PEAK_TFLOPS = 157.3         # vector fp32 spec (FMA = 2 FLOP)
-FP32_NOFMA_TFLOPS = 78.6         # 256 CU x 128 lanes x 2.4 GHz, one mul/add per lane-cycle
+# fp32 VALU: 256 CU x 4 SIMD x 32 lanes/clk x 2.4 GHz = 78.6 T lane-ops/s; the 157.3 TFLOP/s spec
+# counts an FMA as 2 FLOP.  The path is built with -ffp-contract=off (parity), so its adds and
+# multiplies issue one per lane-cycle: 78.6 T is its ceiling, 157.3 T the FMA figure.
+FP32_NOFMA_TFLOPS = 78.6
+FP32_PEAK_TFLOPS = 157.3
 
 
 def flop_per_sample(w):
@@ -50,34 +70,76 @@ def flop_per_sample(w):
             + FLOP["diffuse"] * w["diffuse"] + FLOP["refr"] * w["refr"] + FLOP["per_sample"])
 
 
-def cpu_baseline(sp, cam, W, H, sid, vlp, seconds):
-    """The oracle (CPU restatement) on this host's cores: a bounded sample of the same frame."""
-    import numpy as np
+def host_cpus():
+    """The CPUs this process may use: affinity mask, capped by a cgroup CPU quota if one is set."""
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = nproc
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    usable = aff if quota is None else max(1, min(aff, int(quota)))
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"nproc": nproc, "affinity": aff, "cgroup_quota_cpus": quota, "threads": usable, "model": model}
+
+
+def cpu_baseline(sp, cam, W, H, rows, sid, vlp, seconds):
+    """The oracle (CPU restatement) on every CPU this job may use: a bounded sample of the same
+    workload (its pixel region `rows`, the same sids), plus a 1-core figure."""
     import oracle
 
-    threads = min(16, os.cpu_count() or 1)
+    cpus = host_cpus()
+    threads = cpus["threads"]
     rnd = oracle.mt607(0)
     lp = oracle.light_pass(sp, rnd, 0)
+    y0, y1 = rows
+    cal = (y0, min(y1, y0 + 32))                      # calibration: one pass over 32 rows
     t = time.perf_counter()
-    oracle.path_passes(sp, rnd, cam, W, H, lp, sid[:1], vlp[:1], nthreads=threads)
-    t_pass = time.perf_counter() - t
-    npass = max(1, min(len(sid), int(round(seconds / max(t_pass, 1e-3)))))
+    oracle.path_passes(sp, rnd, cam, W, H, lp, sid[:1], vlp[:1], rows=cal, nthreads=threads)
+    rate = (cal[1] - cal[0]) * W / max(time.perf_counter() - t, 1e-4)
+    target = rate * seconds
+    region = (y1 - y0) * W
+    if target >= region:
+        npass, ry = max(1, min(len(sid), int(target // region))), (y0, y1)
+    else:
+        npass, ry = 1, (y0, y0 + max(8, int(target // W)))
     t = time.perf_counter()
-    oracle.path_passes(sp, rnd, cam, W, H, lp, sid[:npass], vlp[:npass], nthreads=threads)
+    oracle.path_passes(sp, rnd, cam, W, H, lp, sid[:npass], vlp[:npass], rows=ry, nthreads=threads)
     dt = time.perf_counter() - t
-    # one core: every 4th 16-row band, one pass
+    value = (ry[1] - ry[0]) * W * npass / dt / 1e6
+    # one core: every 4th 8-row band of the region, one pass
     t1, n1 = 0.0, 0
-    for y0 in range(0, H, 64):
-        y1 = min(H, y0 + 16)
+    for b0 in range(y0, y1, 32):
+        b1 = min(y1, b0 + 8)
         t = time.perf_counter()
-        oracle.path_passes(sp, rnd, cam, W, H, lp, sid[:1], vlp[:1], rows=(y0, y1), nthreads=1)
+        oracle.path_passes(sp, rnd, cam, W, H, lp, sid[:1], vlp[:1], rows=(b0, b1), nthreads=1)
         t1 += time.perf_counter() - t
-        n1 += (y1 - y0) * W
-    return {"value": W * H * npass / dt / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/ CPU restatement, full {W}x{H} cornell frame x {npass} passes "
-                      f"(same sids as the GPU), OpenMP {threads} threads; 1-core: every 4th 16-row "
-                      f"band x 1 pass",
-            "value_1core": n1 / t1 / 1e6, "seconds": round(dt, 2)}
+        n1 += (b1 - b0) * W
+        if t1 > seconds / 3:
+            break
+    v1 = n1 / t1 / 1e6
+    return {"value": round(value, 3), "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/ CPU restatement (OpenMP, {threads} threads = every CPU this job may use), "
+                      f"rows {ry[0]}..{ry[1]} of the {W}x{H} frame x {npass} passes (same sids as the GPU); "
+                      f"1-core: every 4th 8-row band x 1 pass",
+            "seconds": round(dt, 2), "value_1core": round(v1, 4),
+            "nproc": cpus["nproc"], "affinity_cpus": cpus["affinity"], "cgroup_quota_cpus": cpus["cgroup_quota_cpus"],
+            "cpu_model": cpus["model"],
+            "node_linear_estimate": round(v1 * cpus["nproc"], 2),
+            "node_linear_estimate_note": "1-core rate x nproc: an upper bound for the whole host (perfect scaling)"}
 
 
 def main():
@@ -85,11 +147,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--scene", default="cornell")
-    ap.add_argument("--width", type=int, default=1920, help="CLI width (internal = +1)")
-    ap.add_argument("--height", type=int, default=1080, help="CLI height (internal = +1)")
-    ap.add_argument("--passes", type=int, default=32, help="passes per step per GPU share")
-    ap.add_argument("--band-rows", type=int, default=8)
+    ap.add_argument("--workload", default="cornell1080", choices=sorted(WORKLOADS))
+    ap.add_argument("--scene", default=None, help="override the workload's scene (same frame layout)")
+    ap.add_argument("--width", type=int, default=None, help="CLI width (internal = +1)")
+    ap.add_argument("--height", type=int, default=None, help="CLI height (internal = +1)")
+    ap.add_argument("--passes", type=int, default=None, help="passes per step (per GPU share for weak scaling)")
+    ap.add_argument("--band-rows", type=int, default=None)
     ap.add_argument("--traversal", default="auto", choices=["auto", "brute", "bvh"],
                     help="sphere traversal for >16-sphere scenes (results identical)")
     ap.add_argument("--streams", type=int, default=0, help="pass streams per pixel (0 = auto)")
@@ -100,6 +163,10 @@ def main():
     ap.add_argument("--rehearse", action="store_true",
                     help="multi-rank dry run on fewer GPUs: gloo, ranks share devices (not a measurement)")
     args = ap.parse_args()
+    wl = dict(WORKLOADS[args.workload])
+    for k in ("scene", "width", "height", "passes", "band_rows"):
+        if getattr(args, k) is not None:
+            wl[k] = getattr(args, k)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -120,19 +187,26 @@ def main():
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    W, H = args.width + 1, args.height + 1                   # smallpt_cpu.c:409-410
-    cam, sp = g.read_scene(os.path.join(REPO, "assets", "scenes", args.scene + ".scn"))
+    W, H = wl["width"] + 1, wl["height"] + 1                 # smallpt_cpu.c:409-410
+    band = wl["band_rows"]
+    nshards = wl["fixed_bands"] or world                     # weak64: 8 fixed bands, rank r renders band r
+    if world > nshards:
+        raise SystemExit(f"workload {args.workload} has {nshards} bands: at most {nshards} ranks")
+    cam, sp = g.read_scene(os.path.join(REPO, "assets", "scenes", wl["scene"] + ".scn"))
     g.update_camera(cam, W, H)
     r = g.Renderer(sp, W, H, cam, device=local)
-    r.set_shard(rank, world, args.band_rows)
+    r.set_shard(rank, nshards, band)
     r.set_traversal(args.traversal)
     r.set_streams(args.streams)
     r.set_specialize(bool(args.specialize))
     r.light_pass(0)                                           # UpdateRendering2
     sched = g.PassScheduler()
     sched.light()
-    per_step = args.passes * world
+    per_step = wl["passes"] * (world if (wl["scaling"] == "weak" and not wl["fixed_bands"]) else 1)
     sid, vlp = sched.next(per_step * (args.warmup + args.steps))
+    # samples per step over the whole job: every owned pixel of every rank, once per pass
+    job_pixels = sum(shd.owned_pixels(W, H, q, nshards, band) for q in range(world))
+    own_pixels = shd.owned_pixels(W, H, rank, nshards, band)
 
     def step(k):
         a, b = k * per_step, (k + 1) * per_step
@@ -170,19 +244,19 @@ def main():
 
     kern_ms, _ = r.kernel_timing()                            # path kernels alone
     dev_ms, launches = r.path_timing()                        # + the pass-stream fold
-    samples = W * H * per_step * args.steps                   # every pixel exactly once per pass
+    samples = job_pixels * per_step * args.steps
     value = samples / dt / 1e6
 
     if rank == 0:
         if dist is not None:
             r.update_pixels()
-            cnt = t_cnt.cpu().numpy()
-            assert (cnt == per_step * (args.warmup + args.steps)).all(), "reduced counters wrong"
-        own_pixels = shd.owned_pixels(W, H, rank, world, args.band_rows)
-        w = WORK.get(args.scene)
+            cnt = t_cnt.cpu().numpy().reshape(H, W)
+            owned = (torch.arange(H).numpy() // band) % nshards < world
+            assert (cnt[owned] == per_step * (args.warmup + args.steps)).all(), "reduced counters wrong"
+        w = WORK.get(wl["scene"])
         avg_launch_s = kern_ms / 1e3 / max(launches, 1)
         passes_per_launch = per_step * args.steps / max(launches, 1)
-        roofline = valu = None
+        roofline = None
         if w is not None:
             samples_per_launch = own_pixels * passes_per_launch
             if r.last_streams > 1:
@@ -191,58 +265,67 @@ def main():
                 bytes_per_launch = own_pixels * 4 + samples_per_launch * (4 * w["rng_reads"] + 12)
             else:
                 bytes_per_launch = own_pixels * ACCUM_BYTES_PER_PIXEL + samples_per_launch * 4 * w["rng_reads"]
-            achieved = bytes_per_launch / avg_launch_s / 1e9
+            gbs = bytes_per_launch / avg_launch_s / 1e9
+            fl = flop_per_sample(w) * samples_per_launch / avg_launch_s / 1e12
             traffic = None
             pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
-            if os.path.exists(pmc):
+            if os.path.exists(pmc) and world == 1:
                 rec = json.load(open(pmc))
-                if rec.get("scene") == args.scene and rec.get("passes_per_launch") == passes_per_launch \
+                if rec.get("workload", "cornell1080") == args.workload and rec.get("scene") == wl["scene"] \
+                        and rec.get("passes_per_launch") == passes_per_launch \
                         and rec.get("pass_streams") in (None, r.last_streams) \
                         and rec.get("specialized", False) == r.last_specialized \
-                        and rec.get("width") == W and rec.get("height") == H and world == 1:
+                        and rec.get("width") == W and rec.get("height") == H:
                     traffic = rec.get("hbm_bytes_per_launch")
-            roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                        "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                        "bytes_per_launch": int(bytes_per_launch), "avg_launch_ms": round(avg_launch_s * 1e3, 4),
-                        "launches": launches}
-            fl = flop_per_sample(w) * samples_per_launch / avg_launch_s / 1e12
-            valu = {"achieved": round(fl, 2), "unit": "TFLOP/s", "peak": FP32_PEAK_TFLOPS,
-                    "frac": round(fl / FP32_PEAK_TFLOPS, 4), "peak_no_fma": FP32_NOFMA_TFLOPS,
-                    "frac_no_fma": round(fl / FP32_NOFMA_TFLOPS, 4),
-                    "flop_per_sample": round(flop_per_sample(w), 1),
-                    "note": "bound: fp32 VALU (no contraction, correctly rounded div/sqrt); "
-                            "FLOP model in DESIGN.md"}
+            roofline = {"bound": "valu", "achieved": round(fl, 3), "peak": FP32_NOFMA_TFLOPS, "unit": "TFLOP/s",
+                        "frac": round(fl / FP32_NOFMA_TFLOPS, 4), "traffic": traffic,
+                        "peak_fma": FP32_PEAK_TFLOPS, "frac_fma": round(fl / FP32_PEAK_TFLOPS, 4),
+                        "flop_per_sample": round(flop_per_sample(w), 1),
+                        "samples_per_launch": int(samples_per_launch),
+                        "avg_launch_ms": round(avg_launch_s * 1e3, 4), "launches": launches,
+                        "hbm": {"achieved": round(gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                "frac": round(gbs / HBM_PEAK_GBS, 5), "bytes_per_launch": int(bytes_per_launch)},
+                        "note": "fp32 VALU bound: -ffp-contract=off, so one add or mul per lane-cycle (78.6 T/s); "
+                                "FLOP model and per-sample bytes in DESIGN.md; traffic = calibrated PMC "
+                                "FETCH_SIZE+WRITE_SIZE per launch (profiles/pmc_traffic.json)"}
             pv = os.path.join(REPO, "profiles", "pmc_valu.json")
             if os.path.exists(pv) and world == 1:
                 rec = json.load(open(pv))
-                if rec.get("scene") == args.scene and rec.get("passes_per_launch") == passes_per_launch \
+                if rec.get("scene") == wl["scene"] and rec.get("passes_per_launch") == passes_per_launch \
                         and rec.get("pass_streams") == r.last_streams and rec.get("width") == W \
                         and rec.get("specialized", False) == r.last_specialized:
-                    valu["busy_pmc"] = rec["valu_busy"]
-                    valu["lane_utilisation_pmc"] = rec["valu_lane_utilisation"]
+                    roofline["valu_busy_pmc"] = rec["valu_busy"]
+                    roofline["lane_utilisation_pmc"] = rec["valu_lane_utilisation"]
             if r.last_traversal == "bvh":
-                valu["note"] = ("reference-equivalent FLOPs: the reference tests every sphere; the BVH "
-                                "skips most tests, so this is work avoided, not VALU throughput")
+                roofline["note"] = ("reference-equivalent FLOPs: the reference tests every sphere; the BVH "
+                                    "skips most tests, so this is work avoided, not VALU throughput")
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(sp, cam, W, H, sid, vlp, args.cpu_seconds)
+            rows = shd.owned_row_ranges(H, rank, nshards, band)
+            region = (rows[0][0], rows[0][1]) if wl["fixed_bands"] else (0, H)
+            cpu = cpu_baseline(sp, cam, W, H, region, sid, vlp, args.cpu_seconds)
         line = {
             "metric": METRIC, "value": round(value, 2), "unit": "Msamples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
-            "data": "synthetic: reference cornell.scn + MT607 table (seed 0) + glibc-rand pass offsets",
-            "config": {"workload": f"{args.scene}.scn {W}x{H} internal (CLI {args.width}x{args.height}), "
-                                   f"<=7-segment eye paths + NEE + 1 VLP per diffuse vertex",
-                       "scene": args.scene, "width": W, "height": H, "passes_per_step": per_step,
+            "higher_is_better": True, "scaling": wl["scaling"], "vs_baseline": None, "dtype": "fp32",
+            "data": f"synthetic: reference {wl['scene']}.scn + MT607 table (seed 0) + glibc-rand pass offsets",
+            "config": {"workload": f"{args.workload}: {wl['scene']}.scn {W}x{H} internal "
+                                   f"(CLI {wl['width']}x{wl['height']}), <=7-segment eye paths + NEE + 1 VLP "
+                                   f"per diffuse vertex; {wl['config']}",
+                       "scene": wl["scene"], "width": W, "height": H, "passes_per_step": per_step,
+                       "samples_per_step": job_pixels * per_step,
                        "spp_total": per_step * (args.warmup + args.steps),
-                       "parallelism": f"pixel bands x{world} ({args.band_rows}-row, interleaved)",
+                       "parallelism": (f"{nshards} fixed {band}-row bands, rank r renders band r" if wl["fixed_bands"]
+                                       else f"pixel bands x{world} ({band}-row, interleaved)"),
                        "pass_streams": r.last_streams, "traversal": r.last_traversal,
                        "specialized": r.last_specialized},
             "device_ms_per_step": round(dev_ms / args.steps, 3),
-            "roofline": roofline, "valu": valu, "cpu_baseline": cpu,
+            "roofline": roofline, "cpu_baseline": cpu,
+            "host": {"gpu": torch.cuda.get_device_name(local), "hostname": socket.gethostname()},
         }
         if cpu:
             line["speedup_vs_cpu"] = round(value / cpu["value"], 1)
+            line["speedup_vs_cpu_node_linear_estimate"] = round(value / cpu["node_linear_estimate"], 1)
         if args.rehearse:
             line["rehearsal"] = "ranks share GPUs over gloo: exercises the multi-rank flow, not a measurement"
         print(json.dumps(line), flush=True)

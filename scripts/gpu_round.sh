@@ -41,8 +41,13 @@ for s in $STEPS; do
     for sc in ${SCENES_LIST:-cornell cornell_glass caustic simple synthetic64}; do
       timeout -k 10 300 python bench.py --no-cpu-baseline --scene $sc ${BENCH_ARGS:-} > gpurun_out/scene_$sc.log 2>&1
       rc=$?; echo "scene $sc rc=$rc $(tail -1 gpurun_out/scene_$sc.log | cut -c1-90)"
-      python -c "import json; d=json.loads(open('gpurun_out/scene_$sc.log').read().strip().splitlines()[-1]); print('   ', d['value'], 'Msamples/s', d['device_ms_per_step'], 'ms/step', 'valu', d['valu']['achieved'] if d['valu'] else None)" || true
+      python -c "import json; d=json.loads(open('gpurun_out/scene_$sc.log').read().strip().splitlines()[-1]); print('   ', d['value'], 'Msamples/s', d['device_ms_per_step'], 'ms/step', 'valu TF', d['roofline']['achieved'] if d['roofline'] else None)" || true
       ok_or_stop $rc scene_$sc
+    done ;;
+  workloads)
+    for w in ${WORKLOADS_LIST:-caustic8 weak64}; do
+      timeout -k 10 400 python bench.py --workload $w --cpu-seconds 6 > gpurun_out/wl_$w.log 2>&1
+      rc=$?; echo "workload $w rc=$rc"; tail -1 gpurun_out/wl_$w.log | cut -c1-400; ok_or_stop $rc wl_$w
     done ;;
   shard)
     timeout -k 10 400 python scripts/shard_probe.py ${SHARD_ARGS:-} > gpurun_out/shard_probe.log 2>&1
@@ -62,7 +67,7 @@ for s in $STEPS; do
     i=0
     for set in "${PMC_SETS[@]}"; do
       i=$((i+1)); P=gpurun_out/${PMC_OUT:-pmc}; rm -rf $P$i; mkdir -p $(dirname $P)
-      timeout -k 10 300 rocprofv3 --pmc $set --kernel-trace -d $P$i -o run --output-format csv -- \
+      timeout -s KILL 240 rocprofv3 --pmc $set --kernel-trace -d $P$i -o run --output-format csv -- \
           python3 bench.py --no-cpu-baseline --steps 4 --warmup 1 ${BENCH_ARGS:-} > $P$i.log 2>&1
       rc=$?; echo "pmc set $i ($set): rc=$rc"; tail -1 $P$i.log; ok_or_stop $rc pmc$i
     done ;;

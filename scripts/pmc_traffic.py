@@ -56,7 +56,7 @@ for f in sorted(glob.glob(os.path.join(root, "pmc*.log"))):
         d = json.loads(lines[-1])
         cfg, roof = d["config"], d.get("roofline") or {}
         break
-rec = {"scene": cfg.get("scene", "cornell"), "width": cfg.get("width", 1921), "height": cfg.get("height", 1081),
+rec = {"workload": cfg.get("workload", "cornell1080").split(":")[0], "scene": cfg.get("scene", "cornell"), "width": cfg.get("width", 1921), "height": cfg.get("height", 1081),
        "passes_per_launch": float(cfg.get("passes_per_step", 16)), "pass_streams": cfg.get("pass_streams"), "specialized": cfg.get("specialized", False),
        "fetch_reported_bytes_per_launch": int(fetch), "write_reported_bytes_per_launch": int(write),
        "fetch_scale": fscale, "write_scale": wscale,
