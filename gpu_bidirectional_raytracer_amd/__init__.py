@@ -158,12 +158,19 @@ class Renderer:
     """One C-ABI context (bdpt_create): device buffers, MT table, VLPs and the accumulation."""
 
     def __init__(self, spheres, width: int, height: int, camera: Optional[Camera] = None,
-                 dat_path: str = DEFAULT_DAT, device: int = 0):
+                 dat_path: str = DEFAULT_DAT, device: int = 0, devices: Optional[Sequence[int]] = None):
+        """devices=[d0, d1, ...]: one multi-device context (bdpt_create_multi): pixel bands over
+        the devices, frame assembled on d0 (RCCL when the devices are distinct)."""
         self.width, self.height = int(width), int(height)
         self.spheres = spheres_to_array(spheres)
         h = ctypes.c_void_p()
-        rc = lib.bdpt_create(ctypes.byref(h), _sphere_ptr(self.spheres), len(self.spheres),
-                             self.width, self.height, os.fsencode(dat_path), int(device))
+        if devices is not None:
+            devs = np.ascontiguousarray(devices, dtype=np.int32)
+            rc = lib.bdpt_create_multi(ctypes.byref(h), _sphere_ptr(self.spheres), len(self.spheres),
+                                       self.width, self.height, os.fsencode(dat_path), _ptr(devs), len(devs))
+        else:
+            rc = lib.bdpt_create(ctypes.byref(h), _sphere_ptr(self.spheres), len(self.spheres),
+                                 self.width, self.height, os.fsencode(dat_path), int(device))
         if rc != BDPT_OK:
             raise BdptError(rc, lib.bdpt_create_error().decode())
         self._h = h
@@ -239,6 +246,18 @@ class Renderer:
     @property
     def last_traversal(self) -> str:
         return {1: "brute", 2: "bvh"}[int(lib.bdpt_last_traversal(self._h))]
+
+    @property
+    def num_devices(self) -> int:
+        return int(lib.bdpt_num_devices(self._h))
+
+    @property
+    def reduce_backend(self) -> str:
+        """'rccl' / 'peer' for a multi-device context, 'none' for a one-device context."""
+        return lib.bdpt_reduce_backend(self._h).decode()
+
+    def reduce_frame(self) -> None:
+        self._chk(lib.bdpt_reduce_frame(self._h))
 
     # -- work
     def generate_rand(self, seed: int) -> None:

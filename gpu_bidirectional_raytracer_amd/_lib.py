@@ -60,6 +60,11 @@ _P = ctypes.c_void_p
 _SIGS = [
     ("bdpt_create", ctypes.c_int, [ctypes.POINTER(_P), ctypes.POINTER(Sphere), ctypes.c_uint,
                                     ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]),
+    ("bdpt_create_multi", ctypes.c_int, [ctypes.POINTER(_P), ctypes.POINTER(Sphere), ctypes.c_uint,
+                                          ctypes.c_int, ctypes.c_int, ctypes.c_char_p, _P, ctypes.c_int]),
+    ("bdpt_num_devices", ctypes.c_int, [_P]),
+    ("bdpt_reduce_backend", ctypes.c_char_p, [_P]),
+    ("bdpt_reduce_frame", ctypes.c_int, [_P]),
     ("bdpt_destroy", None, [_P]),
     ("bdpt_last_error", ctypes.c_char_p, [_P]),
     ("bdpt_create_error", ctypes.c_char_p, []),

@@ -8,6 +8,7 @@
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
+#include <rccl/rccl.h>                 // types and prototypes only: librccl is opened with dlopen
 #include <math.h>
 #include <stdarg.h>
 #include <stdio.h>
@@ -39,6 +40,7 @@ extern "C" __global__ void bdpt_light_kernel(const bdpt_dev_sphere*, unsigned, c
 extern "C" const void* bdpt_path_kernel_table[36];   // [(S > 1) * 18 + (BVH ? 17 : n <= 16 ? n : 0)]
 extern "C" __global__ void bdpt_pixels_kernel(const bdpt_dev_vec*, uchar4*, const float*, int);
 extern "C" __global__ void bdpt_accum_kernel(bdpt_path_args);
+extern "C" __global__ void bdpt_frame_add_kernel(float*, const float*, unsigned*, const unsigned*, int);
 
 // gamma thresholds (host, once): see bdpt_util.c
 extern "C" void bdpt_gamma_thresholds(float thr[256]);
@@ -106,7 +108,21 @@ struct bdpt_ctx {
     char jit_err[256] = {0};            // why the last specialisation fell back (diagnostics)
     int jit_waves = 0;                  // waves/SIMD bound of the last specialised build
     char err[512] = {0};
+    // multi-device context (bdpt_create_multi): this context renders on devices[0] and owns the
+    // peer contexts of the other devices; the frame is assembled on devices[0] by a sum-reduce
+    bool multi = false;
+    std::vector<bdpt_ctx*> peers;
+    std::vector<void*> comms;           // ncclComm_t per device when the reduce runs on RCCL
+    int reduce_mode = 0;                // kReduce*
+    bool frame_stale = true;            // the assembled frame predates the last change
+    bdpt_dev_vec* d_fcolors = nullptr;  // assembled frame (devices[0])
+    unsigned* d_fcounter = nullptr;
+    uchar4* d_fpixels = nullptr;
+    bdpt_dev_vec* d_ftmp = nullptr;     // peer-copy staging (kReducePeer)
+    unsigned* d_ftmpc = nullptr;
+    char reduce_note[160] = {0};        // why RCCL is not used, if it is not
 };
+enum { kReduceNone = 0, kReduceRccl = 1, kReducePeer = 2 };
 
 static int fail(bdpt_ctx* c, int code, const char* fmt, ...) {
     if (c) {
@@ -220,7 +236,8 @@ static int upload_scene(bdpt_ctx* c) {
 static void release(bdpt_ctx* c) {
     void* bufs[] = {c->d_params, c->d_rand, c->d_lp, c->d_sph, c->d_lights, c->d_geom, c->d_lightrec, c->d_colors,
                     c->d_counter, c->d_pixels, c->d_thr, c->d_pass, c->d_rbuf, c->d_bvh_nodes,
-                    c->d_bvh_geom, c->d_big_geom, c->d_mat, c->d_bvh_ids, c->d_big_ids};
+                    c->d_bvh_geom, c->d_big_geom, c->d_mat, c->d_bvh_ids, c->d_big_ids,
+                    c->d_fcolors, c->d_fcounter, c->d_fpixels, c->d_ftmp, c->d_ftmpc};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (auto& s : c->ring) {
@@ -559,36 +576,39 @@ int bdpt_create(bdpt_ctx** out, const bdpt_sphere* spheres, unsigned n, int W, i
 
 const char* bdpt_create_error(void) { return g_create_err; }
 
+static void destroy_group(bdpt_ctx* c);
+
 void bdpt_destroy(bdpt_ctx* c) {
     if (!c) return;
+    destroy_group(c);
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     release(c);
     delete c;
 }
 
-int bdpt_set_scene(bdpt_ctx* c, const bdpt_sphere* spheres, unsigned n) {
+static int one_set_scene(bdpt_ctx* c, const bdpt_sphere* spheres, unsigned n) {
     if (!c || (n > 0 && !spheres)) return BDPT_EINVAL;
     HIPCHK(c, hipSetDevice(c->device));
     c->spheres.assign(spheres, spheres + n);
     return upload_scene(c);
 }
 
-int bdpt_set_camera(bdpt_ctx* c, const bdpt_camera* cam) {
+static int one_set_camera(bdpt_ctx* c, const bdpt_camera* cam) {
     if (!c || !cam) return BDPT_EINVAL;
     c->cam = *cam;
     c->cam_set = true;
     return BDPT_OK;
 }
 
-int bdpt_reset_accum(bdpt_ctx* c) {
+static int one_reset_accum(bdpt_ctx* c) {
     if (!c) return BDPT_EINVAL;
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipMemsetAsync(c->d_counter, 0, sizeof(unsigned) * (size_t)c->W * c->H, c->stream));
     return BDPT_OK;
 }
 
-int bdpt_set_shard(bdpt_ctx* c, int shard, int nshards, int band_rows) {
+static int one_set_shard(bdpt_ctx* c, int shard, int nshards, int band_rows) {
     if (!c || nshards < 1 || shard < 0 || shard >= nshards || band_rows < 1)
         return c ? fail(c, BDPT_EINVAL, "bdpt_set_shard: bad shard %d/%d band %d", shard, nshards, band_rows)
                  : BDPT_EINVAL;
@@ -596,7 +616,7 @@ int bdpt_set_shard(bdpt_ctx* c, int shard, int nshards, int band_rows) {
     return BDPT_OK;
 }
 
-int bdpt_set_streams(bdpt_ctx* c, int streams) {
+static int one_set_streams(bdpt_ctx* c, int streams) {
     if (!c) return BDPT_EINVAL;
     if (streams < 0 || streams > BDPT_MAX_STREAMS)
         return fail(c, BDPT_EINVAL, "bdpt_set_streams: bad stream count %d", streams);
@@ -606,7 +626,7 @@ int bdpt_set_streams(bdpt_ctx* c, int streams) {
 
 int bdpt_last_streams(const bdpt_ctx* c) { return c ? c->last_streams : BDPT_EINVAL; }
 
-int bdpt_set_specialize(bdpt_ctx* c, int on) {
+static int one_set_specialize(bdpt_ctx* c, int on) {
     if (!c) return BDPT_EINVAL;
     c->specialize = on != 0;
     return BDPT_OK;
@@ -616,7 +636,7 @@ int bdpt_last_specialized(const bdpt_ctx* c) { return c ? (int)c->last_specializ
 
 const char* bdpt_specialize_status(const bdpt_ctx* c) { return c ? c->jit_err : "null context"; }
 
-int bdpt_set_traversal(bdpt_ctx* c, int mode) {
+static int one_set_traversal(bdpt_ctx* c, int mode) {
     if (!c) return BDPT_EINVAL;
     if (mode != BDPT_TRAVERSE_AUTO && mode != BDPT_TRAVERSE_BRUTE && mode != BDPT_TRAVERSE_BVH)
         return fail(c, BDPT_EINVAL, "bdpt_set_traversal: bad mode %d", mode);
@@ -630,7 +650,7 @@ int bdpt_last_traversal(const bdpt_ctx* c) {
     return c ? (c->last_bvh ? BDPT_TRAVERSE_BVH : BDPT_TRAVERSE_BRUTE) : BDPT_EINVAL;
 }
 
-int bdpt_generate_rand(bdpt_ctx* c, unsigned seed) {
+static int one_generate_rand(bdpt_ctx* c, unsigned seed) {
     if (!c) return BDPT_EINVAL;
     HIPCHK(c, hipSetDevice(c->device));
     // seedMTGPU(seed): every record's seed field := seed (MersenneTwister_kernel.cu:44-47)
@@ -645,13 +665,13 @@ int bdpt_generate_rand(bdpt_ctx* c, unsigned seed) {
     return BDPT_OK;
 }
 
-int bdpt_light_pass(bdpt_ctx* c, int current_sample) {
+static int one_light_pass(bdpt_ctx* c, int current_sample) {
     if (!c) return BDPT_EINVAL;
     // The reference regenerates the table per light with the same seed (smallpt_cpu.c:321-322):
     // one generation is identical.  With no emitter it launches nothing and the path pass reads
     // an uninitialised d_Rand; we generate the table anyway (the frame is black either way:
     // there is no emission, and dev_lp stays zero) so the run is defined.
-    int rc = bdpt_generate_rand(c, (unsigned)(current_sample * 5));
+    int rc = one_generate_rand(c, (unsigned)(current_sample * 5));
     if (rc) return rc;
     if (c->lights.empty()) return BDPT_OK;
     hipLaunchKernelGGL(bdpt_light_kernel, dim3(BDPT_LIGHT_POINTS / 64), dim3(64), 0, c->stream,
@@ -668,7 +688,7 @@ static void vnorm3(float v[3]) {
     v[0] = l * v[0]; v[1] = l * v[1]; v[2] = l * v[2];
 }
 
-int bdpt_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int npass) {
+static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int npass) {
     if (!c) return BDPT_EINVAL;
     if (npass < 0 || (npass > 0 && (!sid || !vlp))) return fail(c, BDPT_EINVAL, "bdpt_path_passes: bad pass list");
     if (npass == 0) return BDPT_OK;
@@ -744,6 +764,12 @@ int bdpt_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int npass
         const int owned = c->shard < nbands ? (nbands - c->shard + c->nshards - 1) / c->nshards : 0;
         a.tiles_per_band = tpb;
         grid_rows = owned * tpb;
+        // only the frame's last band can be partial: launch none of its tile rows below the frame
+        if (owned > 0) {
+            const int last = c->shard + (owned - 1) * c->nshards;          // this shard's last band
+            const int tail = (last + 1) * tpb - tile_rows;
+            if (tail > 0) grid_rows -= tail;
+        }
     }
     // Pass streams: auto = one pass per lane (S = the launch's pass count).  Eye paths are capped
     // at 7 segments and most reach the cap, so single-path lanes keep a wave almost perfectly
@@ -850,7 +876,7 @@ int bdpt_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int npass
     return BDPT_OK;
 }
 
-int bdpt_synchronize(bdpt_ctx* c) {
+static int one_synchronize(bdpt_ctx* c) {
     if (!c) return BDPT_EINVAL;
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -859,31 +885,31 @@ int bdpt_synchronize(bdpt_ctx* c) {
 
 int bdpt_last_path_ms(bdpt_ctx* c, float* ms) {
     if (!c || !ms) return BDPT_EINVAL;
-    if (int rc = bdpt_synchronize(c)) return rc;
+    if (int rc = one_synchronize(c)) return rc;
     if (c->acc_launches == 0) return fail(c, BDPT_ESTATE, "bdpt_last_path_ms: no path pass launched");
     *ms = c->last_ms;
     return BDPT_OK;
 }
 
-int bdpt_path_timing(bdpt_ctx* c, double* total_ms, long long* launches, int reset) {
+static int one_path_timing(bdpt_ctx* c, double* total_ms, long long* launches, int reset) {
     if (!c) return BDPT_EINVAL;
-    if (int rc = bdpt_synchronize(c)) return rc;
+    if (int rc = one_synchronize(c)) return rc;
     if (total_ms) *total_ms = c->acc_ms;
     if (launches) *launches = c->acc_launches;
     if (reset) { c->acc_ms = 0.0; c->acc_kernel_ms = 0.0; c->acc_launches = 0; }
     return BDPT_OK;
 }
 
-int bdpt_kernel_timing(bdpt_ctx* c, double* kernel_ms, long long* launches, int reset) {
+static int one_kernel_timing(bdpt_ctx* c, double* kernel_ms, long long* launches, int reset) {
     if (!c) return BDPT_EINVAL;
-    if (int rc = bdpt_synchronize(c)) return rc;
+    if (int rc = one_synchronize(c)) return rc;
     if (kernel_ms) *kernel_ms = c->acc_kernel_ms;
     if (launches) *launches = c->acc_launches;
     if (reset) { c->acc_ms = 0.0; c->acc_kernel_ms = 0.0; c->acc_launches = 0; }
     return BDPT_OK;
 }
 
-int bdpt_read_radiance(bdpt_ctx* c, bdpt_vec* colors, unsigned* counter) {
+static int one_read_radiance(bdpt_ctx* c, bdpt_vec* colors, unsigned* counter) {
     if (!c) return BDPT_EINVAL;
     HIPCHK(c, hipSetDevice(c->device));
     const size_t np = (size_t)c->W * c->H;
@@ -893,7 +919,7 @@ int bdpt_read_radiance(bdpt_ctx* c, bdpt_vec* colors, unsigned* counter) {
     return BDPT_OK;
 }
 
-int bdpt_read_pixels(bdpt_ctx* c, unsigned char* rgba) {
+static int one_read_pixels(bdpt_ctx* c, unsigned char* rgba) {
     if (!c || !rgba) return BDPT_EINVAL;
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipMemcpyAsync(rgba, c->d_pixels, 4 * (size_t)c->W * c->H, hipMemcpyDeviceToHost, c->stream));
@@ -918,7 +944,7 @@ int bdpt_read_lightpaths(bdpt_ctx* c, bdpt_lightpath* lp) {
     return BDPT_OK;
 }
 
-int bdpt_device_buffers(bdpt_ctx* c, void** colors, void** counter, void** pixels) {
+static int one_device_buffers(bdpt_ctx* c, void** colors, void** counter, void** pixels) {
     if (!c) return BDPT_EINVAL;
     if (colors) *colors = c->d_colors;
     if (counter) *counter = c->d_counter;
@@ -926,7 +952,7 @@ int bdpt_device_buffers(bdpt_ctx* c, void** colors, void** counter, void** pixel
     return BDPT_OK;
 }
 
-int bdpt_update_pixels(bdpt_ctx* c) {
+static int one_update_pixels(bdpt_ctx* c) {
     if (!c) return BDPT_EINVAL;
     HIPCHK(c, hipSetDevice(c->device));
     const int np = c->W * c->H;
@@ -938,3 +964,311 @@ int bdpt_update_pixels(bdpt_ctx* c) {
 }
 
 }  // extern "C"
+
+// ---- multi-device contexts (SURVEY.md 8(b) `devices[], ndev`; 5: RCCL in one process) --------
+// bdpt_create_multi makes one context per device: the first renders on devices[0] and owns the
+// others (peers).  Device k renders the 8-row bands (y / 8) % ndev == k; every other entry point
+// applies to all devices (each rebuilds the MT table and the VLPs itself: they are deterministic),
+// and the read-back entry points first assemble the frame on devices[0]: an in-process RCCL
+// ncclReduce (sum) of the float radiance and the counters over ncclCommInitAll's communicator
+// (the sum is exact, each pixel is non-zero on one device only), or, when the devices are not
+// distinct (several shards on one GPU) or RCCL is unavailable, peer copies plus an add kernel.
+namespace {
+struct rccl_api {
+    bool ok = false;
+    decltype(&ncclCommInitAll) init_all = nullptr;
+    decltype(&ncclCommDestroy) destroy = nullptr;
+    decltype(&ncclReduce) reduce = nullptr;
+    decltype(&ncclGroupStart) group_start = nullptr;
+    decltype(&ncclGroupEnd) group_end = nullptr;
+    decltype(&ncclGetErrorString) errstr = nullptr;
+};
+
+const rccl_api& rccl() {
+    static const rccl_api api = [] {
+        rccl_api r;
+        // torch (when loaded) has mapped its own librccl.so.1 already: the same SONAME binds to it
+        const char* libs[] = {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"};
+        void* h = nullptr;
+        for (const char* l : libs)
+            if ((h = dlopen(l, RTLD_NOW | RTLD_LOCAL))) break;
+        if (!h) return r;
+        r.init_all = (decltype(r.init_all))dlsym(h, "ncclCommInitAll");
+        r.destroy = (decltype(r.destroy))dlsym(h, "ncclCommDestroy");
+        r.reduce = (decltype(r.reduce))dlsym(h, "ncclReduce");
+        r.group_start = (decltype(r.group_start))dlsym(h, "ncclGroupStart");
+        r.group_end = (decltype(r.group_end))dlsym(h, "ncclGroupEnd");
+        r.errstr = (decltype(r.errstr))dlsym(h, "ncclGetErrorString");
+        r.ok = r.init_all && r.destroy && r.reduce && r.group_start && r.group_end && r.errstr;
+        return r;
+    }();
+    return api;
+}
+}  // namespace
+
+static void destroy_group(bdpt_ctx* c) {
+    if (!c->multi) return;
+    for (bdpt_ctx* p : c->peers) {
+        (void)hipSetDevice(p->device);
+        if (p->stream) (void)hipStreamSynchronize(p->stream);
+    }
+    if (!c->comms.empty() && rccl().ok)
+        for (void* cm : c->comms) (void)rccl().destroy((ncclComm_t)cm);
+    c->comms.clear();
+    for (bdpt_ctx* p : c->peers) bdpt_destroy(p);
+    c->peers.clear();
+}
+
+// Apply `f` to every peer; the first failure is reported on the group context.
+template <class F>
+static int forward(bdpt_ctx* c, F f) {
+    for (bdpt_ctx* p : c->peers)
+        if (int rc = f(p)) return fail(c, rc, "device %d: %s", p->device, p->err);
+    c->frame_stale = true;
+    return BDPT_OK;
+}
+
+// Group shard layout: device k of a group that is shard `shard` of `nshards` groups renders
+// shard shard * ndev + k of nshards * ndev.
+static int group_set_shard(bdpt_ctx* c, int shard, int nshards, int band_rows) {
+    const int ndev = 1 + (int)c->peers.size();
+    if (int rc = one_set_shard(c, shard * ndev, nshards * ndev, band_rows)) return rc;
+    for (int k = 1; k < ndev; k++)
+        if (int rc = one_set_shard(c->peers[k - 1], shard * ndev + k, nshards * ndev, band_rows))
+            return fail(c, rc, "device %d: %s", c->peers[k - 1]->device, c->peers[k - 1]->err);
+    c->frame_stale = true;
+    return BDPT_OK;
+}
+
+// Assemble the frame of a multi-device context on devices[0] (d_fcolors/d_fcounter/d_fpixels).
+static int assemble(bdpt_ctx* c) {
+    if (!c->multi || !c->frame_stale) return BDPT_OK;
+    if (int rc = one_synchronize(c)) return rc;
+    for (bdpt_ctx* p : c->peers)
+        if (int rc = one_synchronize(p)) return fail(c, rc, "device %d: %s", p->device, p->err);
+    const size_t np = (size_t)c->W * c->H;
+    HIPCHK(c, hipSetDevice(c->device));
+    if (!c->d_fcolors) {
+        HIPCHK(c, hipMalloc(&c->d_fcolors, sizeof(bdpt_dev_vec) * np));
+        HIPCHK(c, hipMalloc(&c->d_fcounter, sizeof(unsigned) * np));
+        HIPCHK(c, hipMalloc(&c->d_fpixels, sizeof(uchar4) * np));
+    }
+    if (c->reduce_mode == kReduceRccl) {
+        const rccl_api& api = rccl();
+        ncclResult_t r = api.group_start();
+        for (size_t k = 0; r == ncclSuccess && k < c->comms.size(); k++) {
+            bdpt_ctx* d = k == 0 ? c : c->peers[k - 1];
+            HIPCHK(c, hipSetDevice(d->device));
+            r = api.reduce(d->d_colors, k == 0 ? (void*)c->d_fcolors : (void*)d->d_colors, 3 * np, ncclFloat32,
+                           ncclSum, 0, (ncclComm_t)c->comms[k], d->stream);
+            if (r == ncclSuccess)
+                r = api.reduce(d->d_counter, k == 0 ? (void*)c->d_fcounter : (void*)d->d_counter, np, ncclUint32,
+                               ncclSum, 0, (ncclComm_t)c->comms[k], d->stream);
+        }
+        const ncclResult_t e = api.group_end();
+        if (r == ncclSuccess) r = e;
+        if (r != ncclSuccess) return fail(c, BDPT_EHIP, "ncclReduce: %s", api.errstr(r));
+        for (size_t k = 1; k < c->comms.size(); k++) {
+            HIPCHK(c, hipSetDevice(c->peers[k - 1]->device));
+            HIPCHK(c, hipStreamSynchronize(c->peers[k - 1]->stream));
+        }
+        HIPCHK(c, hipSetDevice(c->device));
+    } else {
+        HIPCHK(c, hipMemcpyAsync(c->d_fcolors, c->d_colors, sizeof(bdpt_dev_vec) * np, hipMemcpyDeviceToDevice, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->d_fcounter, c->d_counter, sizeof(unsigned) * np, hipMemcpyDeviceToDevice, c->stream));
+        if (!c->peers.empty() && !c->d_ftmp) {
+            HIPCHK(c, hipMalloc(&c->d_ftmp, sizeof(bdpt_dev_vec) * np));
+            HIPCHK(c, hipMalloc(&c->d_ftmpc, sizeof(unsigned) * np));
+        }
+        for (bdpt_ctx* p : c->peers) {
+            HIPCHK(c, hipMemcpyPeerAsync(c->d_ftmp, c->device, p->d_colors, p->device, sizeof(bdpt_dev_vec) * np, c->stream));
+            HIPCHK(c, hipMemcpyPeerAsync(c->d_ftmpc, c->device, p->d_counter, p->device, sizeof(unsigned) * np, c->stream));
+            hipLaunchKernelGGL(bdpt_frame_add_kernel, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, c->stream,
+                               (float*)c->d_fcolors, (const float*)c->d_ftmp, c->d_fcounter,
+                               (const unsigned*)c->d_ftmpc, (int)np);
+            HIPCHK(c, hipGetLastError());
+        }
+    }
+    hipLaunchKernelGGL(bdpt_pixels_kernel, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, c->stream,
+                       (const bdpt_dev_vec*)c->d_fcolors, c->d_fpixels, (const float*)c->d_thr, (int)np);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->frame_stale = false;
+    return BDPT_OK;
+}
+
+extern "C" {
+
+int bdpt_create_multi(bdpt_ctx** out, const bdpt_sphere* spheres, unsigned n, int W, int H,
+                      const char* mt_dat_path, const int* devices, int ndev) {
+    if (!out) return BDPT_EINVAL;
+    *out = nullptr;
+    if (!devices || ndev < 1 || ndev > 64) {
+        snprintf(g_create_err, sizeof g_create_err, "bdpt_create_multi: bad device list (%d devices)", ndev);
+        return BDPT_EINVAL;
+    }
+    bdpt_ctx* c = nullptr;
+    if (int rc = bdpt_create(&c, spheres, n, W, H, mt_dat_path, devices[0])) return rc;
+    c->multi = true;
+    for (int k = 1; k < ndev; k++) {
+        bdpt_ctx* p = nullptr;
+        if (int rc = bdpt_create(&p, spheres, n, W, H, mt_dat_path, devices[k])) {
+            char msg[512];
+            snprintf(msg, sizeof msg, "device %d: %s", devices[k], g_create_err);
+            bdpt_destroy(c);
+            snprintf(g_create_err, sizeof g_create_err, "%s", msg);
+            return rc;
+        }
+        c->peers.push_back(p);
+    }
+    if (int rc = group_set_shard(c, 0, 1, 8)) {
+        snprintf(g_create_err, sizeof g_create_err, "%s", c->err);
+        bdpt_destroy(c);
+        return rc;
+    }
+    // RCCL when every device is distinct (a communicator holds each GPU once), else peer copies
+    bool distinct = true;
+    for (int a = 0; a < ndev; a++)
+        for (int b = a + 1; b < ndev; b++) distinct = distinct && devices[a] != devices[b];
+    const char* force = getenv("BDPT_REDUCE");
+    c->reduce_mode = kReducePeer;
+    if (force && !strcmp(force, "peer")) {
+        snprintf(c->reduce_note, sizeof c->reduce_note, "BDPT_REDUCE=peer");
+    } else if (!distinct) {
+        snprintf(c->reduce_note, sizeof c->reduce_note, "devices repeat: peer copies");
+    } else if (!rccl().ok) {
+        snprintf(c->reduce_note, sizeof c->reduce_note, "librccl not found: peer copies");
+    } else {
+        std::vector<ncclComm_t> comms(ndev);
+        const ncclResult_t r = rccl().init_all(comms.data(), ndev, devices);
+        if (r == ncclSuccess) {
+            c->comms.assign(comms.begin(), comms.end());
+            c->reduce_mode = kReduceRccl;
+        } else {
+            snprintf(c->reduce_note, sizeof c->reduce_note, "ncclCommInitAll: %s: peer copies", rccl().errstr(r));
+        }
+    }
+    (void)hipSetDevice(devices[0]);
+    *out = c;
+    return BDPT_OK;
+}
+
+int bdpt_num_devices(const bdpt_ctx* c) { return c ? 1 + (int)c->peers.size() : BDPT_EINVAL; }
+
+const char* bdpt_reduce_backend(const bdpt_ctx* c) {
+    if (!c) return "null context";
+    if (!c->multi) return "none";
+    return c->reduce_mode == kReduceRccl ? "rccl" : "peer";
+}
+
+int bdpt_reduce_frame(bdpt_ctx* c) {
+    if (!c) return BDPT_EINVAL;
+    return assemble(c);
+}
+
+// ---- the entry points: this context, then (multi-device) every peer ------------------------
+int bdpt_set_scene(bdpt_ctx* c, const bdpt_sphere* spheres, unsigned n) {
+    if (int rc = one_set_scene(c, spheres, n)) return rc;
+    return forward(c, [&](bdpt_ctx* p) { return one_set_scene(p, spheres, n); });
+}
+int bdpt_set_camera(bdpt_ctx* c, const bdpt_camera* cam) {
+    if (int rc = one_set_camera(c, cam)) return rc;
+    return forward(c, [&](bdpt_ctx* p) { return one_set_camera(p, cam); });
+}
+int bdpt_reset_accum(bdpt_ctx* c) {
+    if (int rc = one_reset_accum(c)) return rc;
+    return forward(c, [&](bdpt_ctx* p) { return one_reset_accum(p); });
+}
+int bdpt_set_shard(bdpt_ctx* c, int shard, int nshards, int band_rows) {
+    if (!c) return BDPT_EINVAL;
+    if (!c->multi) return one_set_shard(c, shard, nshards, band_rows);
+    if (nshards < 1 || shard < 0 || shard >= nshards || band_rows < 1)
+        return fail(c, BDPT_EINVAL, "bdpt_set_shard: bad shard %d/%d band %d", shard, nshards, band_rows);
+    return group_set_shard(c, shard, nshards, band_rows);
+}
+int bdpt_set_streams(bdpt_ctx* c, int streams) {
+    if (int rc = one_set_streams(c, streams)) return rc;
+    return forward(c, [&](bdpt_ctx* p) { return one_set_streams(p, streams); });
+}
+int bdpt_set_specialize(bdpt_ctx* c, int on) {
+    if (int rc = one_set_specialize(c, on)) return rc;
+    return forward(c, [&](bdpt_ctx* p) { return one_set_specialize(p, on); });
+}
+int bdpt_set_traversal(bdpt_ctx* c, int mode) {
+    if (int rc = one_set_traversal(c, mode)) return rc;
+    return forward(c, [&](bdpt_ctx* p) { return one_set_traversal(p, mode); });
+}
+int bdpt_generate_rand(bdpt_ctx* c, unsigned seed) {
+    if (int rc = one_generate_rand(c, seed)) return rc;
+    return forward(c, [&](bdpt_ctx* p) { return one_generate_rand(p, seed); });
+}
+int bdpt_light_pass(bdpt_ctx* c, int current_sample) {
+    if (int rc = one_light_pass(c, current_sample)) return rc;
+    return forward(c, [&](bdpt_ctx* p) { return one_light_pass(p, current_sample); });
+}
+// Every device's passes are queued before any is waited for: the devices render concurrently.
+int bdpt_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int npass) {
+    if (int rc = one_path_passes(c, sid, vlp, npass)) return rc;
+    return forward(c, [&](bdpt_ctx* p) { return one_path_passes(p, sid, vlp, npass); });
+}
+int bdpt_synchronize(bdpt_ctx* c) {
+    if (int rc = one_synchronize(c)) return rc;
+    for (bdpt_ctx* p : c->peers)
+        if (int rc = one_synchronize(p)) return fail(c, rc, "device %d: %s", p->device, p->err);
+    return BDPT_OK;
+}
+// Multi-device: the slowest device's time (the devices run concurrently); launches of devices[0].
+int bdpt_path_timing(bdpt_ctx* c, double* total_ms, long long* launches, int reset) {
+    if (int rc = one_path_timing(c, total_ms, launches, reset)) return rc;
+    for (bdpt_ctx* p : c->peers) {
+        double ms = 0.0;
+        if (int rc = one_path_timing(p, &ms, nullptr, reset)) return fail(c, rc, "device %d: %s", p->device, p->err);
+        if (total_ms && ms > *total_ms) *total_ms = ms;
+    }
+    return BDPT_OK;
+}
+int bdpt_kernel_timing(bdpt_ctx* c, double* kernel_ms, long long* launches, int reset) {
+    if (int rc = one_kernel_timing(c, kernel_ms, launches, reset)) return rc;
+    for (bdpt_ctx* p : c->peers) {
+        double ms = 0.0;
+        if (int rc = one_kernel_timing(p, &ms, nullptr, reset)) return fail(c, rc, "device %d: %s", p->device, p->err);
+        if (kernel_ms && ms > *kernel_ms) *kernel_ms = ms;
+    }
+    return BDPT_OK;
+}
+// Read-back of a multi-device context reads the assembled frame.
+int bdpt_read_radiance(bdpt_ctx* c, bdpt_vec* colors, unsigned* counter) {
+    if (!c) return BDPT_EINVAL;
+    if (!c->multi) return one_read_radiance(c, colors, counter);
+    if (int rc = assemble(c)) return rc;
+    const size_t np = (size_t)c->W * c->H;
+    if (colors) HIPCHK(c, hipMemcpyAsync(colors, c->d_fcolors, sizeof(bdpt_vec) * np, hipMemcpyDeviceToHost, c->stream));
+    if (counter) HIPCHK(c, hipMemcpyAsync(counter, c->d_fcounter, sizeof(unsigned) * np, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return BDPT_OK;
+}
+int bdpt_read_pixels(bdpt_ctx* c, unsigned char* rgba) {
+    if (!c || !rgba) return BDPT_EINVAL;
+    if (!c->multi) return one_read_pixels(c, rgba);
+    if (int rc = assemble(c)) return rc;
+    HIPCHK(c, hipMemcpyAsync(rgba, c->d_fpixels, 4 * (size_t)c->W * c->H, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return BDPT_OK;
+}
+int bdpt_device_buffers(bdpt_ctx* c, void** colors, void** counter, void** pixels) {
+    if (!c) return BDPT_EINVAL;
+    if (!c->multi) return one_device_buffers(c, colors, counter, pixels);
+    if (int rc = assemble(c)) return rc;
+    if (colors) *colors = c->d_fcolors;
+    if (counter) *counter = c->d_fcounter;
+    if (pixels) *pixels = c->d_fpixels;
+    return BDPT_OK;
+}
+int bdpt_update_pixels(bdpt_ctx* c) {
+    if (!c) return BDPT_EINVAL;
+    if (!c->multi) return one_update_pixels(c);
+    return assemble(c);
+}
+
+}  // extern "C"
+

@@ -879,6 +879,21 @@ extern "C" __global__ __launch_bounds__(256) void bdpt_accum_kernel(bdpt_path_ar
     a.pixels[i] = bdpt_dev_to_rgba(col.x, col.y, col.z, a.gamma_thr);
 }
 
+// Frame assembly of a multi-device context without RCCL: add a peer's zero-padded frame (exact:
+// each pixel is non-zero on one device only, and x + 0 == x).
+extern "C" __global__ __launch_bounds__(256) void bdpt_frame_add_kernel(float* __restrict__ col,
+                                                                       const float* __restrict__ add_col,
+                                                                       unsigned* __restrict__ cnt,
+                                                                       const unsigned* __restrict__ add_cnt,
+                                                                       int count) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= count) return;
+    col[3 * i + 0] += add_col[3 * i + 0];
+    col[3 * i + 1] += add_col[3 * i + 1];
+    col[3 * i + 2] += add_col[3 * i + 2];
+    cnt[i] += add_cnt[i];
+}
+
 // Recompute pixels from colors (after a cross-GPU reduce of the radiance frame).
 extern "C" __global__ __launch_bounds__(256) void bdpt_pixels_kernel(const bdpt_dev_vec* __restrict__ colors,
                                                                      uchar4* __restrict__ pixels,

@@ -4,7 +4,7 @@
  * src/display_func.c, with GLUT replaced by a scripted key sequence.
  *
  *   smallpt [<width> <height> <scene.scn>] [--spp N] [--batch B] [--keys KEYS] [--out F.ppm]
- *           [--device D] [--dat PATH]
+ *           [--device D | --gpus N | --devices D0,D1,...] [--tile ROWS] [--seed S] [--dat PATH]
  *
  * Without positional arguments the built-in CornellSpheres scene is used (smallpt_cpu.c:400).
  * Like the reference, width/height get +1 (smallpt_cpu.c:409-410).  The first frame runs the
@@ -13,6 +13,9 @@
  * sphere), 4 6 8 2 9 3 (move the selected sphere), U D L R (arrow keys), P/p (PageUp/Down
  * targets -> here 'P' = PageUp, 'Q' = PageDown), p (SavePPM with the reference's file name);
  * after each key N more passes are rendered.  --p6 writes --out as binary P6.
+ * --gpus N (devices 0..N-1) or --devices LIST renders one frame on several GPUs of this process
+ * (bdpt_create_multi: pixel bands of --tile rows, default 8, frame assembled by an RCCL reduce);
+ * --seed S seeds the pass offsets' rand() (default 1: the reference never calls srand).
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -142,7 +145,9 @@ int main(int argc, char **argv)
 {
     host h;
     memset(&h, 0, sizeof(h));
-    int spp = 16, batch = 64, device = 0, npos = 0, p6 = 0;
+    int spp = 16, batch = 64, device = 0, npos = 0, p6 = 0, ndev = 0, tile = 8;
+    int devices[64];
+    unsigned seed = 1;
     const char *pos[3] = {0, 0, 0}, *out = NULL, *keys = "", *dat = "assets/data/MersenneTwister.dat";
     for (int a = 1; a < argc; a++) {
         if (!strcmp(argv[a], "--spp") && a + 1 < argc) spp = atoi(argv[++a]);
@@ -150,6 +155,16 @@ int main(int argc, char **argv)
         else if (!strcmp(argv[a], "--keys") && a + 1 < argc) keys = argv[++a];
         else if (!strcmp(argv[a], "--out") && a + 1 < argc) out = argv[++a];
         else if (!strcmp(argv[a], "--device") && a + 1 < argc) device = atoi(argv[++a]);
+        else if (!strcmp(argv[a], "--gpus") && a + 1 < argc) {
+            ndev = atoi(argv[++a]);
+            if (ndev < 1 || ndev > 64) { fprintf(stderr, "--gpus: 1..64\n"); return 1; }
+            for (int k = 0; k < ndev; k++) devices[k] = k;
+        } else if (!strcmp(argv[a], "--devices") && a + 1 < argc) {
+            ndev = 0;
+            for (char *t = strtok(argv[++a], ","); t && ndev < 64; t = strtok(NULL, ",")) devices[ndev++] = atoi(t);
+            if (ndev < 1) { fprintf(stderr, "--devices: empty list\n"); return 1; }
+        } else if (!strcmp(argv[a], "--tile") && a + 1 < argc) tile = atoi(argv[++a]);
+        else if (!strcmp(argv[a], "--seed") && a + 1 < argc) seed = (unsigned)strtoul(argv[++a], NULL, 10);
         else if (!strcmp(argv[a], "--dat") && a + 1 < argc) dat = argv[++a];
         else if (!strcmp(argv[a], "--p6")) p6 = 1;
         else if (npos < 3) pos[npos++] = argv[a];
@@ -175,12 +190,18 @@ int main(int argc, char **argv)
     h.width += 1;
     bdpt_update_camera(&h.camera, h.width, h.height);
     bdpt_pass_state_init(&h.ps);
+    if (seed != 1) bdpt_srand(&h.ps.rng, seed);
 
     fprintf(stderr, "Allocate Buffers\n");
-    int rc = bdpt_create(&h.ctx, h.spheres, h.n, h.width, h.height, dat, device);
+    int rc = ndev ? bdpt_create_multi(&h.ctx, h.spheres, h.n, h.width, h.height, dat, devices, ndev)
+                  : bdpt_create(&h.ctx, h.spheres, h.n, h.width, h.height, dat, device);
     if (rc != BDPT_OK) {
         fprintf(stderr, "Unable to allocate GPU data: %s\n", bdpt_create_error());
         return 1;
+    }
+    if (ndev) {
+        report(&h, bdpt_set_shard(h.ctx, 0, 1, tile), "bands");
+        fprintf(stderr, "Devices: %d, frame reduce: %s\n", bdpt_num_devices(h.ctx), bdpt_reduce_backend(h.ctx));
     }
     report(&h, bdpt_set_camera(h.ctx, &h.camera), "camera");
 

@@ -57,6 +57,22 @@ typedef struct bdpt_ctx bdpt_ctx;
  * `device` is the HIP ordinal this context renders on. Accumulation starts zeroed. */
 int  bdpt_create(bdpt_ctx **out, const bdpt_sphere *spheres, unsigned n_spheres,
                  int width, int height, const char *mt_dat_path, int device);
+/* Multi-GPU context (SURVEY.md 8(b) `bdpt_create(..., devices, ndev)`; the reference renders on
+ * one device, smallpt_cpu.c:422).  One sub-context per entry of devices[]: device k renders the
+ * 8-row pixel bands (y / 8) % ndev == k, every other entry point below applies to all devices,
+ * and the read-back entry points (bdpt_read_radiance / _pixels, bdpt_device_buffers,
+ * bdpt_update_pixels) return the frame assembled on devices[0] by a sum-reduce: an in-process
+ * RCCL ncclReduce over an ncclCommInitAll communicator when the devices are distinct, else peer
+ * copies (several shards on one GPU, or BDPT_REDUCE=peer).  The result equals a one-device
+ * context's bit for bit.  bdpt_set_shard(ctx, s, n, band) makes the whole group shard s of n
+ * groups (multi-node).  bdpt_path_timing / bdpt_kernel_timing report the slowest device. */
+int  bdpt_create_multi(bdpt_ctx **out, const bdpt_sphere *spheres, unsigned n_spheres,
+                       int width, int height, const char *mt_dat_path, const int *devices, int ndev);
+int  bdpt_num_devices(const bdpt_ctx *ctx);
+/* "rccl", "peer", or "none" (a one-device context from bdpt_create). */
+const char *bdpt_reduce_backend(const bdpt_ctx *ctx);
+/* Assemble the frame now (otherwise done on the first read-back after a change). */
+int  bdpt_reduce_frame(bdpt_ctx *ctx);
 /* FreeBuffers smallpt_cpu.c:98-110. */
 void bdpt_destroy(bdpt_ctx *ctx);
 const char *bdpt_last_error(const bdpt_ctx *ctx);
@@ -132,7 +148,8 @@ int  bdpt_read_pixels(bdpt_ctx *ctx, unsigned char *rgba);
 int  bdpt_read_rand(bdpt_ctx *ctx, float *rand_table);          /* d_Rand, BDPT_RAND_N */
 int  bdpt_read_lightpaths(bdpt_ctx *ctx, bdpt_lightpath *lp);   /* dev_lp, 4096        */
 /* Device pointers for zero-copy collectives (RCCL reduce of the radiance frame).  Path passes
- * run asynchronously on the context's own stream: bdpt_synchronize() before using them. */
+ * run asynchronously on the context's own stream: bdpt_synchronize() before using them.  For a
+ * multi-device context: the assembled frame on devices[0]. */
 int  bdpt_device_buffers(bdpt_ctx *ctx, void **colors, void **counter, void **pixels);
 /* Recompute pixels (toInt gamma) from colors on the device, e.g. after a cross-GPU reduce. */
 int  bdpt_update_pixels(bdpt_ctx *ctx);

@@ -171,3 +171,31 @@ def test_create_fails_cleanly_without_gpu():
     assert e.value.code in (_lib.BDPT_EHIP, _lib.BDPT_EIO)
     with pytest.raises(g.BdptError):
         g.Renderer(sp, 17, 9, cam, dat_path="/nonexistent.dat")
+
+
+def test_create_multi_argument_errors():
+    cam, sp = g.read_scene(os.path.join(SCENES, "simple.scn"))
+    arr = g.spheres_to_array(sp)
+    h = ctypes.c_void_p()
+    ptr = ctypes.cast(ctypes.c_void_p(arr.ctypes.data), ctypes.POINTER(_lib.Sphere))
+    devs = np.zeros(2, np.int32)
+    rc = _lib.lib.bdpt_create_multi(ctypes.byref(h), ptr, len(arr), 17, 9, _lib.DEFAULT_DAT.encode(),
+                                    ctypes.c_void_p(devs.ctypes.data), 0)
+    assert rc == _lib.BDPT_EINVAL and not h.value
+    rc = _lib.lib.bdpt_create_multi(ctypes.byref(h), ptr, len(arr), 17, 9, _lib.DEFAULT_DAT.encode(), None, 2)
+    assert rc == _lib.BDPT_EINVAL and b"device list" in _lib.lib.bdpt_create_error()
+    assert _lib.lib.bdpt_reduce_backend(None) == b"null context"
+    assert _lib.lib.bdpt_num_devices(None) == _lib.BDPT_EINVAL
+
+
+def test_create_multi_fails_cleanly_without_gpu():
+    try:
+        import torch
+        if torch.cuda.is_available():
+            pytest.skip("GPU present")
+    except ImportError:
+        pass
+    cam, sp = g.read_scene(os.path.join(SCENES, "simple.scn"))
+    with pytest.raises(g.BdptError) as e:
+        g.Renderer(sp, 17, 9, cam, devices=[0, 1])
+    assert e.value.code == _lib.BDPT_EHIP
