@@ -223,7 +223,7 @@ class Renderer:
         return int(lib.bdpt_last_streams(self._h))
 
     def set_specialize(self, on: bool) -> None:
-        """Scene-specialised kernels (run-time compiled, <= 32 spheres); results are bit-identical."""
+        """Scene-specialised kernels (run-time compiled, <= 64 spheres); results are bit-identical."""
         self._chk(lib.bdpt_set_specialize(self._h, int(bool(on))))
 
     @property

@@ -251,7 +251,7 @@ static void release(bdpt_ctx* c) {
 }
 
 // ---- scene-specialised path kernels (run-time compiled with hipRTC) -------------------------
-// For scenes of <= 32 spheres (not BVH-traversed) the path kernel is recompiled with the scene folded in
+// For scenes of <= 64 spheres (not BVH-traversed) the path kernel is recompiled with the scene folded in
 // (bdpt_kernels.hip BDPT_JIT): the sphere geometry {p, rad^2} as exact hex-float literals and the
 // emitter mask become compile-time constants, so a coordinate difference p - o that several
 // spheres share is formed once per ray (cornell's 9 spheres have 15 distinct coordinates, not
@@ -448,7 +448,12 @@ static hipFunction_t jit_build(bdpt_ctx* c, const std::string& name, const std::
 // nullptr = use the precompiled instance (reason in c->jit_err).
 static hipFunction_t jit_path_kernel(bdpt_ctx* c, bool streams) {
     const unsigned n = (unsigned)c->spheres.size();
-    if (!c->specialize || n < 1 || n > 32) return nullptr;          // kJitEmis is 32 bits
+    if (!c->specialize || n < 1 || n > 64) return nullptr;          // kJitEmis is 64 bits
+    unsigned long long emis = 0;
+    for (unsigned i = 0; i < n; i++) {
+        const bdpt_vec& e = c->spheres[i].e;
+        if (!(e.x == 0.f && e.y == 0.f && e.z == 0.f)) emis |= 1ull << i;
+    }
     if (!rtc().ok) {
         snprintf(c->jit_err, sizeof c->jit_err, "hipRTC not found");
         return nullptr;
@@ -467,7 +472,7 @@ static hipFunction_t jit_path_kernel(bdpt_ctx* c, bool streams) {
         const std::vector<std::string> opts = {
             "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize",
             "-fno-gpu-flush-denormals-to-zero", "-DBDPT_JIT=1", "-DBDPT_JIT_N=" + std::to_string(n),
-            "-DBDPT_JIT_EMIS=" + std::to_string(c->emis_mask) + "u", "-DBDPT_JIT_GEOM=" + geom,
+            "-DBDPT_JIT_EMIS=" + std::to_string(emis) + "ull", "-DBDPT_JIT_GEOM=" + geom,
             "-DBDPT_WAVES_PER_SIMD=" + std::to_string(waves)};
         hipFunction_t fn = jit_build(c, name, opts);
         if (!fn) return nullptr;

@@ -22,7 +22,7 @@
 #ifdef BDPT_JIT
 struct jit_geom { float x, y, z, w; };
 constexpr jit_geom kJitGeom[BDPT_JIT_N] = BDPT_JIT_GEOM;
-constexpr unsigned kJitEmis = BDPT_JIT_EMIS;
+constexpr unsigned long long kJitEmis = BDPT_JIT_EMIS;
 #endif
 
 namespace {
@@ -468,7 +468,7 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
     };
     auto emissive = [&](int s) -> bool {
 #ifdef BDPT_JIT
-        if constexpr (N == BDPT_JIT_N) return (kJitEmis >> s) & 1u;
+        if constexpr (N == BDPT_JIT_N) return (kJitEmis >> s) & 1ull;
 #endif
         if constexpr (N > 0) return (a.emis_mask >> s) & 1u;
         else return (__float_as_int(C[s].w) & 256) != 0;

@@ -100,7 +100,7 @@ int  bdpt_set_streams(bdpt_ctx *ctx, int streams);
 /* S used by the last bdpt_path_passes call. */
 int  bdpt_last_streams(const bdpt_ctx *ctx);
 /* Scene-specialised kernels (no reference counterpart; results are bit-identical): for scenes of
- * <= 32 spheres (brute-force traversal) the path kernel is compiled at run time (hipRTC, ~1 s, cached on disk) with the
+ * <= 64 spheres (brute-force traversal) the path kernel is compiled at run time (hipRTC, ~1 s, cached on disk) with the
  * sphere geometry folded in as constants.  1 = on (default), 0 = precompiled kernels only.  If
  * hipRTC is unavailable or the compile fails, the precompiled kernel runs. */
 int  bdpt_set_specialize(bdpt_ctx *ctx, int on);

@@ -1,6 +1,6 @@
 """Scene-specialised path kernels (run-time compiled with the sphere geometry folded in,
 bdpt_host.cpp jit_path_kernel) give bit-identical frames to the precompiled kernels, with and
-without pass streams, on every scene kind the specialisation covers (1..32 spheres, one or
+without pass streams, on every scene kind the specialisation covers (1..64 spheres, one or
 several emitters, refractive / specular / diffuse)."""
 import os
 
@@ -32,7 +32,7 @@ def render(name, W, H, npass, specialize, streams, gpu):
 
 
 @pytest.mark.parametrize("name", ["cornell", "cornell_glass", "caustic", "cornell_2luci", "simple",
-                                  "cornell_multi", "hall_of_mirrors", "open"])
+                                  "cornell_multi", "hall_of_mirrors", "open", "synthetic64"])
 @pytest.mark.parametrize("streams", [0, 1])
 def test_specialised_equals_precompiled(gpu, name, streams):
     W, H, npass = 97, 61, 6

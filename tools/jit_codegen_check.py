@@ -39,9 +39,9 @@ def jit_defines(spheres):
     for i, s in enumerate(spheres):
         rr = np.float32(s["rad"]) * np.float32(s["rad"])
         parts.append("{" + ",".join(hexf(x) for x in (s["p"][0], s["p"][1], s["p"][2], rr)) + "}")
-        if i < 32 and any(float(e) != 0.0 for e in s["e"]):
+        if any(float(e) != 0.0 for e in s["e"]):
             emis |= 1 << i
-    return [f"-DBDPT_JIT_N={len(spheres)}", f"-DBDPT_JIT_EMIS={emis}u", "-DBDPT_JIT_GEOM={" + ",".join(parts) + "}"]
+    return [f"-DBDPT_JIT_N={len(spheres)}", f"-DBDPT_JIT_EMIS={emis}ull", "-DBDPT_JIT_GEOM={" + ",".join(parts) + "}"]
 
 
 def scalar_writes(asm):
