@@ -39,6 +39,9 @@ def _load():
                                        ctypes.c_int, ctypes.c_int, P, P, P, ctypes.c_int, P, P, P,
                                        ctypes.c_int, P]
     lib.oracle_path_passes.restype = None
+    lib.oracle_path_span.argtypes = [P, ctypes.c_uint, P, P, ctypes.c_int, ctypes.c_int, ctypes.c_long,
+                                     ctypes.c_long, P, P, P, ctypes.c_int, P, P, P, ctypes.c_int, P]
+    lib.oracle_path_span.restype = None
     lib.oracle_update_camera.argtypes = [P, ctypes.c_int, ctypes.c_int]
     lib.oracle_update_camera.restype = None
     lib.oracle_key_camera.argtypes = [P, ctypes.c_int]
@@ -120,8 +123,9 @@ def special_key(cam: np.ndarray, key: str) -> bool:
 
 
 def path_passes(spheres, rnd, cam, width, height, lp, sid, vlp, colors=None, counter=None,
-                pixels=None, rows=None, nthreads: int = 0, stats: bool = False):
-    """npass x RadiancePathTracingKernel over rows [y0, y1) -> (colors, counter, pixels[, stats])."""
+                pixels=None, rows=None, nthreads: int = 0, stats: bool = False, span=None):
+    """npass x RadiancePathTracingKernel over rows [y0, y1) (or the row-major pixel range
+    span = (p0, p1)) -> (colors, counter, pixels[, stats])."""
     sp = np.ascontiguousarray(spheres.astype(SPHERE_DTYPE, copy=False))
     cam = camera_array(cam)
     sid = np.ascontiguousarray(sid, np.uint32)
@@ -131,9 +135,10 @@ def path_passes(spheres, rnd, cam, width, height, lp, sid, vlp, colors=None, cou
     pixels = np.zeros((height, width, 4), np.uint8) if pixels is None else pixels.copy()
     y0, y1 = (0, height) if rows is None else rows
     st = np.zeros(8, np.uint64)
-    lib.oracle_path_passes(_p(sp), len(sp), _p(rnd), _p(cam), width, height, y0, y1, _p(lp),
-                           _p(sid), _p(vlp), len(sid), _p(colors), _p(counter), _p(pixels),
-                           nthreads, _p(st) if stats else None)
+    p0, p1 = (y0 * width, y1 * width) if span is None else span
+    lib.oracle_path_span(_p(sp), len(sp), _p(rnd), _p(cam), width, height, p0, p1, _p(lp),
+                         _p(sid), _p(vlp), len(sid), _p(colors), _p(counter), _p(pixels),
+                         nthreads, _p(st) if stats else None)
     if stats:
         return colors, counter, pixels, dict(zip(STAT_NAMES, (int(v) for v in st)))
     return colors, counter, pixels

@@ -395,16 +395,35 @@ static Vec path_sample(const Sphere *sp, unsigned n, const float *rnd, const Cam
  * each pixel's passes in order: running mean :774-782, toInt :783-786, counter :787.
  * colors (W*H Vec), counter (W*H), pixels (W*H*4 RGBA) are read-modify-written in place.
  * Returns the statistics of the work done in `stats_out` (8 x uint64) when non-NULL. */
+void oracle_path_span(const Sphere *sp, unsigned n, const float *rnd, const Camera *cam,
+                      int W, int H, long pix0, long pix1, const LightPath *lp,
+                      const unsigned *sid, const int *vlp, int npass,
+                      Vec *colors, unsigned *counter, unsigned char *pixels,
+                      int nthreads, uint64_t *stats_out);
+
 void oracle_path_passes(const Sphere *sp, unsigned n, const float *rnd, const Camera *cam,
                         int W, int H, int y0, int y1, const LightPath *lp,
                         const unsigned *sid, const int *vlp, int npass,
                         Vec *colors, unsigned *counter, unsigned char *pixels,
                         int nthreads, uint64_t *stats_out)
 {
-    const campre cp = camera_pre(cam);
-    ostats tot = {0, 0, 0, 0, 0, 0, 0, 0};
     if (y0 < 0) y0 = 0;
     if (y1 > H) y1 = H;
+    oracle_path_span(sp, n, rnd, cam, W, H, (long)y0 * W, (long)y1 * W, lp, sid, vlp, npass,
+                     colors, counter, pixels, nthreads, stats_out);
+}
+
+/* The same over the row-major pixel range [pix0, pix1) (spot checks of very large frames). */
+void oracle_path_span(const Sphere *sp, unsigned n, const float *rnd, const Camera *cam,
+                      int W, int H, long pix0, long pix1, const LightPath *lp,
+                      const unsigned *sid, const int *vlp, int npass,
+                      Vec *colors, unsigned *counter, unsigned char *pixels,
+                      int nthreads, uint64_t *stats_out)
+{
+    const campre cp = camera_pre(cam);
+    ostats tot = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (pix0 < 0) pix0 = 0;
+    if (pix1 > (long)W * H) pix1 = (long)W * H;
 #ifdef _OPENMP
     if (nthreads > 0) omp_set_num_threads(nthreads);
 #else
@@ -415,7 +434,7 @@ void oracle_path_passes(const Sphere *sp, unsigned n, const float *rnd, const Ca
         ostats loc = {0, 0, 0, 0, 0, 0, 0, 0};
         ostats *st = stats_out ? &loc : NULL;
 #pragma omp for schedule(dynamic, 16)
-        for (long pix = (long)y0 * W; pix < (long)y1 * W; pix++) {
+        for (long pix = pix0; pix < pix1; pix++) {
             const int x = (int)(pix % W), y = (int)(pix / W);
             Vec c = colors[pix];
             unsigned cnt = counter[pix];

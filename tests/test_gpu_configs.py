@@ -4,9 +4,8 @@ configs[1] cornell 513x513, 256 spp      -> whole frame bit-exact vs the oracle
 configs[2] cornell_glass 1921x1081, 1024 spp -> counters, pixel = toInt(colors), oracle rows
 configs[3] caustic 1921x1081, 4096 spp on 8 pixel-band shards -> shard sum == one-context
            frame bit for bit (the RCCL reduce is a sum of disjoint frames), oracle rows
-configs[4] synthetic64 4097x4097 -> one 8-way band shard (what one of 8 GPUs renders) at
-           512 spp: ownership, counters, oracle rows (spp reduced to keep the test short;
-           the vlp_index wrap at 8192 spp is covered by test_counter_cap_30000)
+configs[4] synthetic64 4097x4097 -> one 4097x512 band (what one of 8 GPUs renders) at the
+           full 8192 spp (vlp_index wraps inside the run): ownership, counters, oracle spans
 """
 import os
 
@@ -109,20 +108,30 @@ def test_config3_caustic_1080p_4096spp_8_shards(gpu, rnd0):
         _same(fc[y], ocol[y], f"row {y}")
 
 
-def test_config4_synthetic64_4097_band_shard(gpu, rnd0):
-    W, H, spp, N, rank = 4097, 4097, 512, 8, 3
+def test_config4_synthetic64_4097_band_8192spp(gpu, rnd0):
+    """configs[4] as one GPU of the 8-GPU weak-scaling run renders it (bench.py --workload weak64):
+    the 64-sphere synthetic scene at 4097x4097, one 4097x512 band (rank 3 of 8 fixed bands), the
+    full 8192 spp -- so vlp_index wraps past LIGHT_POINTS inside the run (pass 8190, SURVEY
+    Appendix A.3).  Counters and ownership over the frame, oracle spot checks on 4 pixel spans
+    at the full spp."""
+    W, H, spp, N, rank, band = 4097, 4097, 8192, 8, 3, 512
     r, cam, sp = _setup("synthetic64", W, H, gpu)
     assert len(sp) == 64
-    r.set_shard(rank, N, 8)
+    r.set_shard(rank, N, band)
     sid, vlp = _schedule(spp)
+    assert vlp[8189] == 4095 and vlp[8190] == 0
     r.path_passes(sid, vlp)
     col, cnt = r.read_radiance()
-    owned = (np.arange(H) // 8) % N == rank
+    owned = (np.arange(H) // band) % N == rank
     assert (cnt[owned] == spp).all() and (cnt[~owned] == 0).all()
-    assert np.isfinite(col).all()
+    assert np.isfinite(col).all() and (col[~owned] == 0).all()
+    _pixels_are_toint(r, col)
     lp = oracle.light_pass(sp, rnd0, 0)
-    for y in (24, 2072):                                 # owned rows (band 3 and band 259)
-        assert owned[y]
-        ocol, _, _ = oracle.path_passes(sp, rnd0, cam, W, H, lp, sid, vlp, rows=(y, y + 1))
-        _same(col[y], ocol[y], f"row {y}")
+    y0 = rank * band
+    for y, x in ((y0, 0), (y0 + 200, 2000), (y0 + 377, 4000), (y0 + band - 1, 1500)):
+        p0 = y * W + x
+        p1 = min(p0 + 96, (y + 1) * W)
+        ocol, ocnt, _ = oracle.path_passes(sp, rnd0, cam, W, H, lp, sid, vlp, span=(p0, p1))
+        _same(col.reshape(-1, 3)[p0:p1], ocol.reshape(-1, 3)[p0:p1], f"pixels {p0}..{p1}")
+        _same(cnt.reshape(-1)[p0:p1], ocnt.reshape(-1)[p0:p1], f"counters {p0}..{p1}")
     r.close()
