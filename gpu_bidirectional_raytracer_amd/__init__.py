@@ -12,6 +12,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import struct
 from typing import Optional, Sequence, Tuple
 
 import numpy as np
@@ -304,6 +305,22 @@ class Renderer:
         self._chk(lib.bdpt_read_radiance(self._h, _ptr(col), _ptr(cnt)))
         return col, cnt
 
+    def write_radiance(self, colors: np.ndarray, counter: np.ndarray) -> None:
+        """Upload an accumulation state (the counterpart of read_radiance); pixels follow."""
+        col = np.ascontiguousarray(colors, np.float32).reshape(self.height, self.width, 3)
+        cnt = np.ascontiguousarray(counter, np.uint32).reshape(self.height, self.width)
+        self._chk(lib.bdpt_write_radiance(self._h, _ptr(col), _ptr(cnt)))
+
+    def save_checkpoint(self, path: str, host_state: bytes = b"") -> None:
+        buf = ctypes.create_string_buffer(host_state, len(host_state)) if host_state else None
+        self._chk(lib.bdpt_save_checkpoint(self._h, os.fsencode(path), buf, len(host_state)))
+
+    def load_checkpoint(self, path: str, host_bytes: int = 0) -> bytes:
+        """Restore the accumulation; returns the caller state saved with it (host_bytes long)."""
+        buf = ctypes.create_string_buffer(host_bytes) if host_bytes else None
+        self._chk(lib.bdpt_load_checkpoint(self._h, os.fsencode(path), buf, host_bytes))
+        return buf.raw if buf is not None else b""
+
     def read_pixels(self) -> np.ndarray:
         px = np.empty((self.height, self.width, 4), np.uint8)
         self._chk(lib.bdpt_read_pixels(self._h, _ptr(px)))
@@ -430,6 +447,26 @@ class SmallPT:
 
     def pixels(self) -> np.ndarray:
         return self.renderer.read_pixels()
+
+    _STATE = struct.Struct("<35i3if")          # bdpt_pass_state (31 + f, r, flag, vlp) + 3 ints + float
+
+    def SaveCheckpoint(self, path: str) -> None:
+        """Accumulation + pass schedule + host counters (no reference counterpart)."""
+        st = self.sched.state
+        words = list(st.rng.state) + [st.rng.f, st.rng.r, st.flag, st.vlp_index]
+        blob = self._STATE.pack(*words, self.current_sample, self.reinit_counter, self.current_sphere,
+                                self.total_time)
+        self.renderer.save_checkpoint(path, blob)
+
+    def LoadCheckpoint(self, path: str) -> None:
+        """Restore what SaveCheckpoint wrote; rendering continues bit for bit."""
+        v = self._STATE.unpack(self.renderer.load_checkpoint(path, self._STATE.size))
+        st = self.sched.state
+        for k in range(31):
+            st.rng.state[k] = v[k]
+        st.rng.f, st.rng.r, st.flag, st.vlp_index = v[31:35]
+        self.current_sample, self.reinit_counter, self.current_sphere = v[35:38]
+        self.total_time = v[38]
 
     def SavePPM(self, path: Optional[str] = None, binary: bool = False) -> str:   # smallpt_cpu.c:239-262
         if path is None:

@@ -94,6 +94,9 @@ _SIGS = [
     ("bdpt_read_lightpaths", ctypes.c_int, [_P, _P]),
     ("bdpt_device_buffers", ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.POINTER(_P), ctypes.POINTER(_P)]),
     ("bdpt_update_pixels", ctypes.c_int, [_P]),
+    ("bdpt_write_radiance", ctypes.c_int, [_P, _P, _P]),
+    ("bdpt_save_checkpoint", ctypes.c_int, [_P, ctypes.c_char_p, _P, ctypes.c_uint]),
+    ("bdpt_load_checkpoint", ctypes.c_int, [_P, ctypes.c_char_p, _P, ctypes.c_uint]),
     ("bdpt_read_scene", ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(Camera),
                                         ctypes.POINTER(ctypes.POINTER(Sphere)), ctypes.POINTER(ctypes.c_uint)]),
     ("bdpt_free_scene", None, [ctypes.POINTER(Sphere)]),

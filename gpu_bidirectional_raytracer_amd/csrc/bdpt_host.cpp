@@ -1275,5 +1275,98 @@ int bdpt_update_pixels(bdpt_ctx* c) {
     return assemble(c);
 }
 
+// ---- checkpoint / resume of the accumulation ----------------------------------
+// Upload colors/counter (the counterpart of bdpt_read_radiance) and recompute the pixels.  A
+// multi-device context gives each device only the pixels of its own bands (zeros elsewhere), so
+// the assembled frame is the uploaded one.
+static int one_write_radiance(bdpt_ctx* c, const bdpt_vec* colors, const unsigned* counter, bool masked) {
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const size_t np = (size_t)c->W * c->H;
+    std::vector<bdpt_vec> col;
+    std::vector<unsigned> cnt;
+    if (masked) {
+        col.assign(colors, colors + np);
+        cnt.assign(counter, counter + np);
+        for (int y = 0; y < c->H; y++) {
+            if ((y / c->band_rows) % c->nshards == c->shard) continue;
+            memset(&col[(size_t)y * c->W], 0, sizeof(bdpt_vec) * c->W);
+            memset(&cnt[(size_t)y * c->W], 0, sizeof(unsigned) * c->W);
+        }
+        colors = col.data();
+        counter = cnt.data();
+    }
+    HIPCHK(c, hipMemcpyAsync(c->d_colors, colors, sizeof(bdpt_vec) * np, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->d_counter, counter, sizeof(unsigned) * np, hipMemcpyHostToDevice, c->stream));
+    hipLaunchKernelGGL(bdpt_pixels_kernel, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, c->stream,
+                       (const bdpt_dev_vec*)c->d_colors, c->d_pixels, (const float*)c->d_thr, (int)np);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return BDPT_OK;
+}
+
+int bdpt_write_radiance(bdpt_ctx* c, const bdpt_vec* colors, const unsigned* counter) {
+    if (!c || !colors || !counter) return BDPT_EINVAL;
+    if (int rc = one_write_radiance(c, colors, counter, c->multi)) return rc;
+    return forward(c, [&](bdpt_ctx* p) { return one_write_radiance(p, colors, counter, true); });
+}
+
+namespace {
+const char kCkptMagic[8] = {'B', 'D', 'P', 'T', 'C', 'K', 'P', '1'};
+struct ckpt_header {
+    char magic[8];
+    int width, height;
+    unsigned host_bytes, reserved;
+};
+}  // namespace
+
+int bdpt_save_checkpoint(bdpt_ctx* c, const char* path, const void* host_state, unsigned host_bytes) {
+    if (!c || !path || (host_bytes && !host_state)) return BDPT_EINVAL;
+    const size_t np = (size_t)c->W * c->H;
+    std::vector<bdpt_vec> col(np);
+    std::vector<unsigned> cnt(np);
+    if (int rc = bdpt_read_radiance(c, col.data(), cnt.data())) return rc;
+    ckpt_header h;
+    memcpy(h.magic, kCkptMagic, 8);
+    h.width = c->W; h.height = c->H; h.host_bytes = host_bytes; h.reserved = 0;
+    const std::string tmp = std::string(path) + ".tmp." + std::to_string((long)getpid());
+    FILE* f = fopen(tmp.c_str(), "wb");
+    if (!f) return fail(c, BDPT_EIO, "bdpt_save_checkpoint: cannot open %s", tmp.c_str());
+    bool ok = fwrite(&h, sizeof h, 1, f) == 1 && fwrite(col.data(), sizeof(bdpt_vec), np, f) == np &&
+              fwrite(cnt.data(), sizeof(unsigned), np, f) == np &&
+              (host_bytes == 0 || fwrite(host_state, 1, host_bytes, f) == host_bytes);
+    ok = (fflush(f) == 0) && ok;
+    ok = (fclose(f) == 0) && ok;
+    if (ok) ok = rename(tmp.c_str(), path) == 0;
+    if (!ok) {
+        unlink(tmp.c_str());
+        return fail(c, BDPT_EIO, "bdpt_save_checkpoint: cannot write %s", path);
+    }
+    return BDPT_OK;
+}
+
+int bdpt_load_checkpoint(bdpt_ctx* c, const char* path, void* host_state, unsigned host_bytes) {
+    if (!c || !path || (host_bytes && !host_state)) return BDPT_EINVAL;
+    FILE* f = fopen(path, "rb");
+    if (!f) return fail(c, BDPT_EIO, "bdpt_load_checkpoint: cannot open %s", path);
+    ckpt_header h;
+    const size_t np = (size_t)c->W * c->H;
+    std::vector<bdpt_vec> col(np);
+    std::vector<unsigned> cnt(np);
+    int rc = BDPT_OK;
+    if (fread(&h, sizeof h, 1, f) != 1 || memcmp(h.magic, kCkptMagic, 8) != 0)
+        rc = fail(c, BDPT_EIO, "bdpt_load_checkpoint: %s is not a checkpoint", path);
+    else if (h.width != c->W || h.height != c->H || h.host_bytes != host_bytes)
+        rc = fail(c, BDPT_EINVAL, "bdpt_load_checkpoint: %s holds %dx%d with %u host bytes, not %dx%d with %u",
+                  path, h.width, h.height, h.host_bytes, c->W, c->H, host_bytes);
+    else if (fread(col.data(), sizeof(bdpt_vec), np, f) != np || fread(cnt.data(), sizeof(unsigned), np, f) != np ||
+             (host_bytes && fread(host_state, 1, host_bytes, f) != host_bytes))
+        rc = fail(c, BDPT_EIO, "bdpt_load_checkpoint: %s is truncated", path);
+    fclose(f);
+    if (rc) return rc;
+    return bdpt_write_radiance(c, col.data(), cnt.data());
+}
+
 }  // extern "C"
+
 

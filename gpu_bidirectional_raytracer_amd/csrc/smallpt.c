@@ -16,6 +16,8 @@
  * --gpus N (devices 0..N-1) or --devices LIST renders one frame on several GPUs of this process
  * (bdpt_create_multi: pixel bands of --tile rows, default 8, frame assembled by an RCCL reduce);
  * --seed S seeds the pass offsets' rand() (default 1: the reference never calls srand).
+ * --checkpoint F saves the accumulation and the pass schedule at the end; --resume F restores
+ * them after the first light pass, so a run continues exactly where the saved one stopped.
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -114,6 +116,23 @@ static int save_ppm(host *h, const char *path, int binary)
     return rc;
 }
 
+/* what a checkpoint carries besides the frame: the pass schedule and the host counters */
+typedef struct {
+    bdpt_pass_state ps;
+    int current_sample, reinit_counter, current_sphere;
+    float total_time;
+} host_state;
+
+static void get_state(const host *h, host_state *s)
+{
+    memset(s, 0, sizeof *s);
+    s->ps = h->ps;
+    s->current_sample = h->current_sample;
+    s->reinit_counter = h->reinit_counter;
+    s->current_sphere = h->current_sphere;
+    s->total_time = h->total_time;
+}
+
 static void key(host *h, int k)
 {
     if (k == 'p') {
@@ -149,6 +168,7 @@ int main(int argc, char **argv)
     int devices[64];
     unsigned seed = 1;
     const char *pos[3] = {0, 0, 0}, *out = NULL, *keys = "", *dat = "assets/data/MersenneTwister.dat";
+    const char *ckpt = NULL, *resume = NULL;
     for (int a = 1; a < argc; a++) {
         if (!strcmp(argv[a], "--spp") && a + 1 < argc) spp = atoi(argv[++a]);
         else if (!strcmp(argv[a], "--batch") && a + 1 < argc) batch = atoi(argv[++a]);
@@ -167,6 +187,8 @@ int main(int argc, char **argv)
         else if (!strcmp(argv[a], "--seed") && a + 1 < argc) seed = (unsigned)strtoul(argv[++a], NULL, 10);
         else if (!strcmp(argv[a], "--dat") && a + 1 < argc) dat = argv[++a];
         else if (!strcmp(argv[a], "--p6")) p6 = 1;
+        else if (!strcmp(argv[a], "--checkpoint") && a + 1 < argc) ckpt = argv[++a];
+        else if (!strcmp(argv[a], "--resume") && a + 1 < argc) resume = argv[++a];
         else if (npos < 3) pos[npos++] = argv[a];
         else { fprintf(stderr, "Usage: %s <window width> <window height> <scene file>\n", argv[0]); return -1; }
     }
@@ -207,6 +229,21 @@ int main(int argc, char **argv)
 
     /* IdleFunc display_func.c:192-217: frame 1 = light pass then path pass; then path passes */
     update_rendering2(&h);
+    if (resume) {
+        host_state st;
+        rc = bdpt_load_checkpoint(h.ctx, resume, &st, sizeof st);
+        if (rc != BDPT_OK) {
+            fprintf(stderr, "Resume failed: %s\n", bdpt_last_error(h.ctx));
+            bdpt_destroy(h.ctx);
+            return 1;
+        }
+        h.ps = st.ps;
+        h.current_sample = st.current_sample;
+        h.reinit_counter = st.reinit_counter;
+        h.current_sphere = st.current_sphere;
+        h.total_time = st.total_time;
+        fprintf(stderr, "Resumed at pass %d\n", h.current_sample);
+    }
     for (int done = 0; done < spp; done += batch)
         update_rendering(&h, spp - done < batch ? spp - done : batch);
     for (const char *k = keys; *k; k++) {
@@ -215,6 +252,13 @@ int main(int argc, char **argv)
             update_rendering(&h, spp - done < batch ? spp - done : batch);
     }
     if (out) rc = save_ppm(&h, out, p6);
+    if (ckpt) {
+        host_state st;
+        get_state(&h, &st);
+        const int crc = bdpt_save_checkpoint(h.ctx, ckpt, &st, sizeof st);
+        report(&h, crc, "Checkpoint");
+        if (rc == BDPT_OK) rc = crc;
+    }
     bdpt_destroy(h.ctx);
     if (npos == 3) bdpt_free_scene(h.spheres); else free(h.spheres);
     return rc == BDPT_OK ? 0 : 1;

@@ -154,6 +154,17 @@ int  bdpt_device_buffers(bdpt_ctx *ctx, void **colors, void **counter, void **pi
 /* Recompute pixels (toInt gamma) from colors on the device, e.g. after a cross-GPU reduce. */
 int  bdpt_update_pixels(bdpt_ctx *ctx);
 
+/* ---- checkpoint / resume of the accumulation (no reference counterpart: the reference keeps
+ * it only in dev_colors/dev_counter) ---- */
+/* Upload colors/counter (W*H each; the counterpart of bdpt_read_radiance); pixels are
+ * recomputed.  Rendering then continues from that state bit for bit. */
+int  bdpt_write_radiance(bdpt_ctx *ctx, const bdpt_vec *colors, const unsigned *counter);
+/* File = header {"BDPTCKP1", W, H, host_bytes} + colors + counter + host_bytes of caller state
+ * (e.g. its bdpt_pass_state and current_sample, so the pass schedule resumes too).  Written to a
+ * temporary file and renamed into place.  Load checks W, H and host_bytes against the context. */
+int  bdpt_save_checkpoint(bdpt_ctx *ctx, const char *path, const void *host_state, unsigned host_bytes);
+int  bdpt_load_checkpoint(bdpt_ctx *ctx, const char *path, void *host_state, unsigned host_bytes);
+
 /* ---- host utilities kept for the drop-in (display_func.c / smallpt_cpu.c) ---- */
 
 /* ReadScene display_func.c:112-175. *spheres is malloc'd; free with bdpt_free_scene. */
