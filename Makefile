@@ -36,16 +36,19 @@ $(BUILD)/bdpt_kernels.o: $(CSRC)/bdpt_kernels.hip $(CSRC)/bdpt_device.h $(CSRC)/
 $(CSRC)/bdpt_jit_src.h: tools/embed_jit_sources.py $(CSRC)/bdpt_kernels.hip $(CSRC)/bdpt_device.h $(CSRC)/bdpt_math.h $(CSRC)/bdpt_sincos_table.h
 	python3 tools/embed_jit_sources.py $@
 
-$(BUILD)/bdpt_host.o: $(CSRC)/bdpt_host.cpp $(CSRC)/bdpt_device.h $(CSRC)/bdpt_bvh.h $(CSRC)/bdpt_jit_src.h include/bdpt.h | $(BUILD)
+$(BUILD)/bdpt_host.o: $(CSRC)/bdpt_host.cpp $(CSRC)/bdpt_device.h $(CSRC)/bdpt_bvh.h $(CSRC)/bdpt_cpu.h $(CSRC)/bdpt_jit_src.h include/bdpt.h | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(BUILD)/bdpt_bvh.o: $(CSRC)/bdpt_bvh.cpp $(CSRC)/bdpt_bvh.h include/bdpt.h | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+$(BUILD)/bdpt_cpu.o: $(CSRC)/bdpt_cpu.cpp $(CSRC)/bdpt_cpu.h include/bdpt.h | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
 $(BUILD)/bdpt_util.o: $(CSRC)/bdpt_util.c include/bdpt.h | $(BUILD)
 	$(CC) $(CFLAGS) -c $< -o $@
 
-$(LIB): $(BUILD)/bdpt_kernels.o $(BUILD)/bdpt_host.o $(BUILD)/bdpt_bvh.o $(BUILD)/bdpt_util.o
+$(LIB): $(BUILD)/bdpt_kernels.o $(BUILD)/bdpt_host.o $(BUILD)/bdpt_bvh.o $(BUILD)/bdpt_cpu.o $(BUILD)/bdpt_util.o
 	mkdir -p $(dir $(LIB))
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lm -ldl
 

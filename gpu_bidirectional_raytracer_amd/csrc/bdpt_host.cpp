@@ -23,6 +23,8 @@
 #include "../../include/bdpt.h"
 #include "bdpt_device.h"
 #include "bdpt_bvh.h"
+#include "bdpt_cpu.h"
+#include <chrono>
 
 static_assert(kBvhEmissive == BDPT_DEV_BVH_EMISSIVE, "BVH id flag");
 
@@ -121,6 +123,7 @@ struct bdpt_ctx {
     bdpt_dev_vec* d_ftmp = nullptr;     // peer-copy staging (kReducePeer)
     unsigned* d_ftmpc = nullptr;
     char reduce_note[160] = {0};        // why RCCL is not used, if it is not
+    bdpt_cpu_ctx* cpu = nullptr;        // device == BDPT_DEVICE_CPU: the host backend (bdpt_cpu.cpp)
 };
 enum { kReduceNone = 0, kReduceRccl = 1, kReducePeer = 2 };
 
@@ -542,6 +545,16 @@ int bdpt_create(bdpt_ctx** out, const bdpt_sphere* spheres, unsigned n, int W, i
     size_t got = fread(c->h_params, sizeof(c->h_params), 1, f);
     fclose(f);
     if (got != 1) return (fail(c, BDPT_EIO, "initMTGPU(): failed to load %s", mt_dat_path), bail(BDPT_EIO));
+    if (device == BDPT_DEVICE_CPU) {                          // the host backend: no HIP at all
+        c->cpu = bdpt_cpu_create(spheres, n, W, H, c->h_params);
+        if (!c->cpu) return (fail(c, BDPT_ENOMEM, "bdpt_create: CPU backend allocation"), bail(BDPT_ENOMEM));
+        for (unsigned i = 0; i < n; i++)
+            if (!(spheres[i].e.x == 0.f && spheres[i].e.y == 0.f && spheres[i].e.z == 0.f)) c->lights.push_back((int)i);
+        c->specialize = false;
+        *out = c;
+        return BDPT_OK;
+    }
+    if (device < 0) return (fail(c, BDPT_EINVAL, "bdpt_create: bad device %d", device), bail(BDPT_EINVAL));
 
 #define CK(call) do { hipError_t e_ = (call); if (e_ != hipSuccess) { \
         fail(c, BDPT_EHIP, "%s: %s", #call, hipGetErrorString(e_)); return bail(BDPT_EHIP); } } while (0)
@@ -585,6 +598,11 @@ static void destroy_group(bdpt_ctx* c);
 
 void bdpt_destroy(bdpt_ctx* c) {
     if (!c) return;
+    if (c->cpu) {
+        bdpt_cpu_destroy(c->cpu);
+        delete c;
+        return;
+    }
     destroy_group(c);
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
@@ -594,6 +612,11 @@ void bdpt_destroy(bdpt_ctx* c) {
 
 static int one_set_scene(bdpt_ctx* c, const bdpt_sphere* spheres, unsigned n) {
     if (!c || (n > 0 && !spheres)) return BDPT_EINVAL;
+    if (c->cpu) {
+        c->spheres.assign(spheres, spheres + n);
+        bdpt_cpu_set_scene(c->cpu, spheres, n);
+        return BDPT_OK;
+    }
     HIPCHK(c, hipSetDevice(c->device));
     c->spheres.assign(spheres, spheres + n);
     return upload_scene(c);
@@ -601,6 +624,7 @@ static int one_set_scene(bdpt_ctx* c, const bdpt_sphere* spheres, unsigned n) {
 
 static int one_set_camera(bdpt_ctx* c, const bdpt_camera* cam) {
     if (!c || !cam) return BDPT_EINVAL;
+    if (c->cpu) bdpt_cpu_set_camera(c->cpu, cam);
     c->cam = *cam;
     c->cam_set = true;
     return BDPT_OK;
@@ -608,6 +632,10 @@ static int one_set_camera(bdpt_ctx* c, const bdpt_camera* cam) {
 
 static int one_reset_accum(bdpt_ctx* c) {
     if (!c) return BDPT_EINVAL;
+    if (c->cpu) {
+        bdpt_cpu_reset_accum(c->cpu);
+        return BDPT_OK;
+    }
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipMemsetAsync(c->d_counter, 0, sizeof(unsigned) * (size_t)c->W * c->H, c->stream));
     return BDPT_OK;
@@ -618,6 +646,7 @@ static int one_set_shard(bdpt_ctx* c, int shard, int nshards, int band_rows) {
         return c ? fail(c, BDPT_EINVAL, "bdpt_set_shard: bad shard %d/%d band %d", shard, nshards, band_rows)
                  : BDPT_EINVAL;
     c->shard = shard; c->nshards = nshards; c->band_rows = band_rows;
+    if (c->cpu) bdpt_cpu_set_shard(c->cpu, shard, nshards, band_rows);
     return BDPT_OK;
 }
 
@@ -657,6 +686,11 @@ int bdpt_last_traversal(const bdpt_ctx* c) {
 
 static int one_generate_rand(bdpt_ctx* c, unsigned seed) {
     if (!c) return BDPT_EINVAL;
+    if (c->cpu) {
+        bdpt_cpu_generate_rand(c->cpu, seed);
+        c->rand_ready = true;
+        return BDPT_OK;
+    }
     HIPCHK(c, hipSetDevice(c->device));
     // seedMTGPU(seed): every record's seed field := seed (MersenneTwister_kernel.cu:44-47)
     std::vector<uint32_t> p(c->h_params, c->h_params + 4 * BDPT_MT_RNG_COUNT);
@@ -672,6 +706,11 @@ static int one_generate_rand(bdpt_ctx* c, unsigned seed) {
 
 static int one_light_pass(bdpt_ctx* c, int current_sample) {
     if (!c) return BDPT_EINVAL;
+    if (c->cpu) {
+        bdpt_cpu_light_pass(c->cpu, current_sample);
+        c->rand_ready = true;
+        return BDPT_OK;
+    }
     // The reference regenerates the table per light with the same seed (smallpt_cpu.c:321-322):
     // one generation is identical.  With no emitter it launches nothing and the path pass reads
     // an uninitialised d_Rand; we generate the table anyway (the frame is black either way:
@@ -699,6 +738,19 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
     if (npass == 0) return BDPT_OK;
     if (!c->rand_ready) return fail(c, BDPT_ESTATE, "bdpt_path_passes: no random table (run the light pass first)");
     if (!c->cam_set) return fail(c, BDPT_ESTATE, "bdpt_path_passes: camera not set");
+    if (c->cpu) {                                           // synchronous; wall-clock timing
+        const auto t0 = std::chrono::steady_clock::now();
+        bdpt_cpu_path_passes(c->cpu, sid, vlp, npass);
+        const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        c->last_ms = (float)ms;
+        c->acc_ms += ms;
+        c->acc_kernel_ms += ms;
+        c->acc_launches += 1;
+        c->last_streams = 1;
+        c->last_specialized = false;
+        c->last_bvh = false;
+        return BDPT_OK;
+    }
     HIPCHK(c, hipSetDevice(c->device));
     // this call's ring slot was last used kRing calls ago: wait for (only) that call
     const int slot = (int)(c->issued % bdpt_ctx::kRing);
@@ -883,6 +935,7 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
 
 static int one_synchronize(bdpt_ctx* c) {
     if (!c) return BDPT_EINVAL;
+    if (c->cpu) return BDPT_OK;
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return fold_timing(c);
@@ -916,6 +969,10 @@ static int one_kernel_timing(bdpt_ctx* c, double* kernel_ms, long long* launches
 
 static int one_read_radiance(bdpt_ctx* c, bdpt_vec* colors, unsigned* counter) {
     if (!c) return BDPT_EINVAL;
+    if (c->cpu) {
+        bdpt_cpu_read_radiance(c->cpu, colors, counter);
+        return BDPT_OK;
+    }
     HIPCHK(c, hipSetDevice(c->device));
     const size_t np = (size_t)c->W * c->H;
     if (colors) HIPCHK(c, hipMemcpyAsync(colors, c->d_colors, sizeof(bdpt_vec) * np, hipMemcpyDeviceToHost, c->stream));
@@ -926,6 +983,10 @@ static int one_read_radiance(bdpt_ctx* c, bdpt_vec* colors, unsigned* counter) {
 
 static int one_read_pixels(bdpt_ctx* c, unsigned char* rgba) {
     if (!c || !rgba) return BDPT_EINVAL;
+    if (c->cpu) {
+        bdpt_cpu_read_pixels(c->cpu, rgba);
+        return BDPT_OK;
+    }
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipMemcpyAsync(rgba, c->d_pixels, 4 * (size_t)c->W * c->H, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -935,6 +996,10 @@ static int one_read_pixels(bdpt_ctx* c, unsigned char* rgba) {
 int bdpt_read_rand(bdpt_ctx* c, float* t) {
     if (!c || !t) return BDPT_EINVAL;
     if (!c->rand_ready) return fail(c, BDPT_ESTATE, "bdpt_read_rand: table not generated");
+    if (c->cpu) {
+        bdpt_cpu_read_rand(c->cpu, t);
+        return BDPT_OK;
+    }
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipMemcpyAsync(t, c->d_rand, sizeof(float) * BDPT_RAND_N, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -943,6 +1008,10 @@ int bdpt_read_rand(bdpt_ctx* c, float* t) {
 
 int bdpt_read_lightpaths(bdpt_ctx* c, bdpt_lightpath* lp) {
     if (!c || !lp) return BDPT_EINVAL;
+    if (c->cpu) {
+        bdpt_cpu_read_lightpaths(c->cpu, lp);
+        return BDPT_OK;
+    }
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipMemcpyAsync(lp, c->d_lp, sizeof(bdpt_lightpath) * BDPT_LIGHT_POINTS, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -951,6 +1020,7 @@ int bdpt_read_lightpaths(bdpt_ctx* c, bdpt_lightpath* lp) {
 
 static int one_device_buffers(bdpt_ctx* c, void** colors, void** counter, void** pixels) {
     if (!c) return BDPT_EINVAL;
+    if (c->cpu) return fail(c, BDPT_EINVAL, "bdpt_device_buffers: the CPU backend has no device buffers");
     if (colors) *colors = c->d_colors;
     if (counter) *counter = c->d_counter;
     if (pixels) *pixels = c->d_pixels;
@@ -959,6 +1029,10 @@ static int one_device_buffers(bdpt_ctx* c, void** colors, void** counter, void**
 
 static int one_update_pixels(bdpt_ctx* c) {
     if (!c) return BDPT_EINVAL;
+    if (c->cpu) {
+        bdpt_cpu_update_pixels(c->cpu);
+        return BDPT_OK;
+    }
     HIPCHK(c, hipSetDevice(c->device));
     const int np = c->W * c->H;
     hipLaunchKernelGGL(bdpt_pixels_kernel, dim3((np + 255) / 256), dim3(256), 0, c->stream,
@@ -1108,7 +1182,9 @@ int bdpt_create_multi(bdpt_ctx** out, const bdpt_sphere* spheres, unsigned n, in
                       const char* mt_dat_path, const int* devices, int ndev) {
     if (!out) return BDPT_EINVAL;
     *out = nullptr;
-    if (!devices || ndev < 1 || ndev > 64) {
+    bool has_cpu = false;
+    for (int k = 0; devices && k < ndev && k < 64; k++) has_cpu = has_cpu || devices[k] < 0;
+    if (!devices || ndev < 1 || ndev > 64 || has_cpu) {
         snprintf(g_create_err, sizeof g_create_err, "bdpt_create_multi: bad device list (%d devices)", ndev);
         return BDPT_EINVAL;
     }
@@ -1280,6 +1356,10 @@ int bdpt_update_pixels(bdpt_ctx* c) {
 // multi-device context gives each device only the pixels of its own bands (zeros elsewhere), so
 // the assembled frame is the uploaded one.
 static int one_write_radiance(bdpt_ctx* c, const bdpt_vec* colors, const unsigned* counter, bool masked) {
+    if (c->cpu) {
+        bdpt_cpu_write_radiance(c->cpu, colors, counter);
+        return BDPT_OK;
+    }
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     const size_t np = (size_t)c->W * c->H;

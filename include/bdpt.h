@@ -54,7 +54,10 @@ typedef struct bdpt_ctx bdpt_ctx;
 
 /* AllocateBuffers smallpt_cpu.c:153-237 + loadMTGPU MersenneTwister_kernel.cu:23-36.
  * W,H are the internal sizes AFTER the reference's +1 (smallpt_cpu.c:409-410).
- * `device` is the HIP ordinal this context renders on. Accumulation starts zeroed. */
+ * `device` is the HIP ordinal this context renders on, or BDPT_DEVICE_CPU for the host backend
+ * (the smallpt_cpu.c CPU path: the same render path on the CPU cores, no GPU needed; identical
+ * results; BDPT_CPU_THREADS sets its thread count).  Accumulation starts zeroed. */
+#define BDPT_DEVICE_CPU (-1)
 int  bdpt_create(bdpt_ctx **out, const bdpt_sphere *spheres, unsigned n_spheres,
                  int width, int height, const char *mt_dat_path, int device);
 /* Multi-GPU context (SURVEY.md 8(b) `bdpt_create(..., devices, ndev)`; the reference renders on

@@ -1,0 +1,166 @@
+"""The host (CPU) backend of the C-ABI (bdpt_create with BDPT_DEVICE_CPU = -1, csrc/bdpt_cpu.cpp):
+the reference's CPU-path config (BASELINE.json configs[0]: simple.scn 256x256 CLI, 64 spp) and the
+rest of the render path through the same entry points as the GPU, bit-exact against the oracle and
+the committed golden renders.  Runs without a GPU."""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import gpu_bidirectional_raytracer_amd as g
+import oracle
+from conftest import GOLDEN, REPO, SCENES
+
+CPU = -1
+SMALLPT = os.path.join(REPO, "gpu_bidirectional_raytracer_amd", "smallpt")
+META = json.load(open(os.path.join(GOLDEN, "render_meta.json")))
+
+
+@pytest.fixture(scope="module")
+def rnd0():
+    return oracle.mt607(0)
+
+
+@pytest.fixture(autouse=True)
+def threads(monkeypatch):
+    monkeypatch.setenv("BDPT_CPU_THREADS", "4")
+
+
+def make(name, W, H):
+    cam, sp = g.read_scene(os.path.join(SCENES, name + ".scn"))
+    g.update_camera(cam, W, H)
+    r = g.Renderer(sp, W, H, cam, device=CPU)
+    r.light_pass(0)
+    return r, cam, sp
+
+
+def schedule(n):
+    s = g.PassScheduler()
+    s.light()
+    return s.next(n)
+
+
+def same(a, b, what):
+    assert np.array_equal(np.asarray(a).view(np.uint8), np.asarray(b).view(np.uint8)), what
+
+
+def test_config0_simple_257_64spp_full_frame(rnd0):
+    """configs[0]: simple.scn, CLI 256x256 (internal 257x257), 64 spp, whole frame vs the oracle."""
+    W, H, spp = 257, 257, 64
+    r, cam, sp = make("simple", W, H)
+    sid, vlp = schedule(spp)
+    r.path_passes(sid, vlp)
+    col, cnt = r.read_radiance()
+    lp = oracle.light_pass(sp, rnd0, 0)
+    ocol, ocnt, opx = oracle.path_passes(sp, rnd0, cam, W, H, lp, sid, vlp, nthreads=4)
+    same(cnt, ocnt, "counter")
+    same(col, ocol, "colors")
+    same(r.read_pixels(), opx, "pixels")
+    r.close()
+
+
+def test_mt_table_and_vlps(rnd0):
+    r, cam, sp = make("cornell_2luci", 9, 7)
+    same(r.read_rand(), rnd0, "d_Rand seed 0")
+    same(r.read_lightpaths().view(np.float32), oracle.light_pass(sp, rnd0, 0).view(np.float32), "dev_lp")
+    r.generate_rand(5)
+    same(r.read_rand(), oracle.mt607(5), "d_Rand seed 5")
+    r.close()
+
+
+@pytest.mark.parametrize("name", META["scenes"])
+def test_golden_renders(name):
+    W, H = META["internal_size"]
+    fx = np.load(os.path.join(GOLDEN, f"render_{name}.npz"))
+    r, cam, sp = make(name, W, H)
+    r.path_passes(META["sid"], META["vlp"])
+    col, cnt = r.read_radiance()
+    same(col, fx["colors"], f"colors {name}")
+    same(cnt, fx["counter"], f"counter {name}")
+    same(r.read_pixels(), fx["pixels"], f"pixels {name}")
+    r.close()
+
+
+@pytest.mark.parametrize("name,W,H,npass", [("cornell_glass", 41, 29, 6), ("hall_of_mirrors", 23, 17, 4),
+                                            ("mod_cornell", 9, 7, 2), ("open", 21, 15, 5)])
+def test_more_scenes(rnd0, name, W, H, npass):
+    r, cam, sp = make(name, W, H)
+    sid, vlp = schedule(npass)
+    r.path_passes(sid, vlp)
+    col, cnt = r.read_radiance()
+    ocol, ocnt, _ = oracle.path_passes(sp, rnd0, cam, W, H, oracle.light_pass(sp, rnd0, 0), sid, vlp)
+    same(col, ocol, name)
+    same(cnt, ocnt, name)
+    r.close()
+
+
+def test_shards_reset_checkpoint_and_counter_cap(rnd0, tmp_path):
+    W, H = 31, 26
+    sid, vlp = schedule(6)
+    full, cam, sp = make("cornell", W, H)
+    full.path_passes(sid, vlp)
+    fc, fn = full.read_radiance()
+    acc = np.zeros_like(fc)
+    for k in range(3):                                   # 3 shards of 8-row bands sum to the frame
+        r, _, _ = make("cornell", W, H)
+        r.set_shard(k, 3, 8)
+        r.path_passes(sid, vlp)
+        acc += r.read_radiance()[0]
+        r.close()
+    same(acc, fc, "shard sum")
+    r, _, _ = make("cornell", W, H)                      # checkpoint in the middle
+    r.path_passes(sid[:2], vlp[:2])
+    r.save_checkpoint(str(tmp_path / "c.ckpt"), b"xy")
+    r.close()
+    r, _, _ = make("cornell", W, H)
+    assert r.load_checkpoint(str(tmp_path / "c.ckpt"), 2) == b"xy"
+    r.path_passes(sid[2:], vlp[2:])
+    same(r.read_radiance()[0], fc, "resumed")
+    col = np.ones((H, W, 3), np.float32)                 # the counter < 30000 cap (device.cu:607)
+    cnt = np.full((H, W), 29998, np.uint32)
+    r.write_radiance(col, cnt)
+    r.path_passes(sid, vlp)
+    assert (r.read_radiance()[1] == 30000).all()
+    r.reset_accum()
+    r.path_passes(sid, vlp)
+    same(r.read_radiance()[0], fc, "after reset")
+    with pytest.raises(g.BdptError):
+        r.device_buffers()
+    r.close()
+    full.close()
+
+
+def _read_ppm(path):
+    toks = open(path).read().split()
+    w, h = int(toks[1]), int(toks[2])
+    return np.array(toks[4:], np.int64).reshape(h, w, 3)[::-1]      # file rows are bottom-up
+
+
+def test_smallpt_host_on_cpu_matches_oracle_replay(tmp_path):
+    """The C host with --device -1: camera keys, sphere edits and arrow keys through the CPU
+    backend equal the oracle's restatement of the same session (oracle/replay.py)."""
+    from oracle.replay import Session
+    keys = "wL+4U aQ"
+    names = {"U": "up", "L": "left", "Q": "page_down"}
+    out = tmp_path / "cpu.ppm"
+    env = dict(os.environ, BDPT_CPU_THREADS="4")
+    dat = os.path.join(REPO, "assets", "data", "MersenneTwister.dat")
+    subprocess.check_call([SMALLPT, "24", "18", os.path.join(SCENES, "cornell.scn"), "--spp", "3", "--batch", "2",
+                           "--keys", keys, "--device", "-1", "--out", str(out), "--dat", dat],
+                          cwd=tmp_path, env=env, timeout=300, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    cam, sp = g.read_scene(os.path.join(SCENES, "cornell.scn"))
+    o = np.array([cam.orig.x, cam.orig.y, cam.orig.z], np.float32)
+    t = np.array([cam.target.x, cam.target.y, cam.target.z], np.float32)
+    ora = Session(sp, o, t, 25, 19)
+    for _ in range(3):
+        ora.IdleFunc()
+    for k in keys:
+        if k in names:
+            ora.SpecialFunc(names[k])
+        else:
+            ora.KeyFunc(k)
+        for _ in range(3):
+            ora.IdleFunc()
+    assert np.array_equal(_read_ppm(out), ora.pixels[..., :3].astype(np.int64))
