@@ -58,11 +58,40 @@ $(HOST): $(CSRC)/smallpt.c include/bdpt.h $(LIB)
 $(ORACLE): oracle/bdpt_oracle.c include/bdpt.h
 	$(CC) -O2 -std=gnu11 -fPIC -shared -fopenmp -ffp-contract=off -Wall -o $@ $< -lm
 
+# Sanitizer build (GPU sanitizers are not available on the pool): the C host, the host
+# utilities and the CPU backend under AddressSanitizer + UBSan through a HIP-free context layer,
+# plus the oracle driven against the same CPU backend.  Run by tests/test_asan.py.
+ASAN_FLAGS := -fsanitize=address,undefined -fno-omit-frame-pointer -fno-sanitize-recover=undefined -g -O1 -ffp-contract=off
+ASAN_DIR   := tests/native/_asan
+asan: $(ASAN_DIR)/smallpt_asan $(ASAN_DIR)/oracle_asan
+
+$(ASAN_DIR):
+	mkdir -p $(ASAN_DIR)
+
+$(ASAN_DIR)/%.o: $(CSRC)/%.c include/bdpt.h | $(ASAN_DIR)
+	$(CC) $(ASAN_FLAGS) -std=gnu11 -c $< -o $@
+
+$(ASAN_DIR)/bdpt_cpu.o: $(CSRC)/bdpt_cpu.cpp $(CSRC)/bdpt_cpu.h include/bdpt.h | $(ASAN_DIR)
+	g++ $(ASAN_FLAGS) -std=c++17 -c $< -o $@
+
+$(ASAN_DIR)/asan_cpu_abi.o: tests/native/asan_cpu_abi.cpp $(CSRC)/bdpt_cpu.h include/bdpt.h | $(ASAN_DIR)
+	g++ $(ASAN_FLAGS) -std=c++17 -c $< -o $@
+
+$(ASAN_DIR)/bdpt_oracle.o: oracle/bdpt_oracle.c include/bdpt.h | $(ASAN_DIR)
+	$(CC) $(ASAN_FLAGS) -std=gnu11 -c $< -o $@
+
+$(ASAN_DIR)/smallpt_asan: $(ASAN_DIR)/smallpt.o $(ASAN_DIR)/bdpt_util.o $(ASAN_DIR)/bdpt_cpu.o $(ASAN_DIR)/asan_cpu_abi.o
+	g++ $(ASAN_FLAGS) -o $@ $^ -lm -pthread
+
+$(ASAN_DIR)/oracle_asan: tests/native/oracle_asan.c $(ASAN_DIR)/bdpt_oracle.o $(ASAN_DIR)/bdpt_util.o $(ASAN_DIR)/bdpt_cpu.o $(ASAN_DIR)/asan_cpu_abi.o
+	g++ $(ASAN_FLAGS) -x c -std=gnu11 -c $< -o $(ASAN_DIR)/oracle_asan_main.o
+	g++ $(ASAN_FLAGS) -o $@ $(ASAN_DIR)/oracle_asan_main.o $(filter %.o,$^) -lm -pthread
+
 clean:
-	rm -rf $(BUILD) $(LIB) $(HOST) $(ORACLE) $(CHECKS) $(CSRC)/bdpt_jit_src.h
+	rm -rf $(BUILD) $(LIB) $(HOST) $(ORACLE) $(CHECKS) $(CSRC)/bdpt_jit_src.h $(ASAN_DIR)
 
 # A/B variants for the GPU bench harness: make variant NAME=x EXTRA_HIPFLAGS="..."
 variant:
 	$(MAKE) BUILD=variants/$(NAME)/_build LIB=variants/$(NAME)/libbdpt.so variants/$(NAME)/libbdpt.so
 
-.PHONY: all clean variant
+.PHONY: all clean variant asan
