@@ -477,7 +477,20 @@ static hipFunction_t jit_path_kernel(bdpt_ctx* c, bool streams) {
             "-fno-gpu-flush-denormals-to-zero", "-DBDPT_JIT=1", "-DBDPT_JIT_N=" + std::to_string(n),
             "-DBDPT_JIT_EMIS=" + std::to_string(emis) + "ull", "-DBDPT_JIT_GEOM=" + geom,
             "-DBDPT_WAVES_PER_SIMD=" + std::to_string(waves)};
-        hipFunction_t fn = jit_build(c, name, opts);
+        std::vector<std::string> all = opts;
+        if (const char* extra = getenv("BDPT_JIT_FLAGS")) {    // experiments: extra -D options
+            std::string tok;
+            for (const char* q = extra;; q++) {
+                if (*q == ' ' || *q == 0) {
+                    if (!tok.empty()) all.push_back(tok);
+                    tok.clear();
+                    if (!*q) break;
+                } else {
+                    tok += *q;
+                }
+            }
+        }
+        hipFunction_t fn = jit_build(c, name, all);
         if (!fn) return nullptr;
         int scratch = 0;
         if (hipFuncGetAttribute(&scratch, HIP_FUNC_ATTRIBUTE_LOCAL_SIZE_BYTES, fn) != hipSuccess) {
