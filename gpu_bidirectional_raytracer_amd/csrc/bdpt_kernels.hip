@@ -371,6 +371,10 @@ extern "C" int bdpt_debug_stats(unsigned long long* out, int reset) {
 #ifndef BDPT_WAVES_PER_SIMD
 #define BDPT_WAVES_PER_SIMD 5
 #endif
+// Part-full shadow rounds split the sphere list over lane groups (path kernel, shadow queue).
+#ifndef BDPT_SPLIT_TAIL
+#define BDPT_SPLIT_TAIL 1
+#endif
 // (the specialised build is compiled with -DBDPT_WAVES_PER_SIMD=6: folding the scene in frees
 // registers, and 6 waves/SIMD measured +3 % over 5 on cornell)
 // BVH scenes: 5 waves/SIMD too, although the traversal state spills 10 VGPRs at 96 (measured:
@@ -730,6 +734,37 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                 }
 #endif
                 for (int base = 0; base < total; base += 64) {            // uniform
+#if BDPT_SPLIT_TAIL
+                    // A part-full round (<= 32 rays; typically the second round, ~14 rays for
+                    // cornell) is traced by 2^lg lane groups that split the sphere list: ray r
+                    // goes to lanes r, r + 64/2^lg, ...; group g tests spheres n-1-g, n-1-g-2^lg,
+                    // ...; occlusion is the OR over groups (ballot, folded on the scalar unit).
+                    // Each sphere test is the same float sequence, and occlusion is an OR, so the
+                    // result is the same in any order.
+                    if constexpr (!kBVH) {
+                        const int c = total - base;                        // uniform
+                        int lg = c <= 8 ? 3 : (c <= 16 ? 2 : (c <= 32 ? 1 : 0));
+                        while (lg > 0 && (1 << lg) > n) lg--;
+                        if (lg > 0) {
+                            const int rpg = 64 >> lg;
+                            const int r = lane & (rpg - 1), g = lane >> (6 - lg);
+                            unsigned occ = 0;
+                            if (r < c) {
+                                const float4 r0 = SQ[base + r], r1 = SQ[kQueue + base + r];
+                                const f3 o = mk(r0.x, r0.y, r0.z), d = mk(r1.x, r1.y, r1.z);
+                                const bool vac = r1.w != 0.f;
+                                for (int s = n - 1 - g; s >= 0; s -= 1 << lg) {
+                                    const float dd = sphere_isect_inf(G[s], o, d);
+                                    if (dd < r0.w && !(vac && emissive(s))) { occ = 1; break; }
+                                }
+                            }
+                            unsigned long long m = __builtin_amdgcn_ballot_w64(occ != 0);
+                            for (int w = 32; w >= rpg; w >>= 1) m |= m >> w;   // uniform
+                            if (lane < c) SR[base + lane] = (unsigned)(m >> lane) & 1u;
+                            continue;
+                        }
+                    }
+#endif
                     const int idx = base + lane;
                     if (idx < total) {
                         const float4 r0 = SQ[idx], r1 = SQ[kQueue + idx];
