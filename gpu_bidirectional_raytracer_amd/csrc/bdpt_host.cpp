@@ -497,7 +497,8 @@ static hipFunction_t jit_path_kernel(bdpt_ctx* c, bool streams) {
             (void)hipGetLastError();
             scratch = 0;
         }
-        if (scratch == 0 || waves <= 5) {                    // spill-free, or the 5-wave floor
+        // spill-free, or the 5-wave floor (BDPT_JIT_SCRATCH_OK: keep a spilling build; experiments)
+        if (scratch == 0 || waves <= 5 || getenv("BDPT_JIT_SCRATCH_OK")) {
             c->jit_err[0] = 0;
             c->jit_waves = waves;
             return fn;
@@ -916,12 +917,14 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
 #endif
         const size_t tab = bvh ? tree + a.big_n : 4 * (size_t)a.n;
         const size_t ids = bvh ? tree_ids + a.big_n : 0;
-        const size_t smem = sizeof(float4) * (tab + 3 * (size_t)a.npass + 5 + 4 * 128 * 2)
-                            + sizeof(unsigned) * (4 * 128 + (size_t)a.npass + ids);
-        if (smem > 160 * 1024)
-            return fail(c, BDPT_EINVAL, "bdpt_path_passes: scene too large for LDS (%u spheres)", a.n);
         // S per launch: a short last chunk gets no idle stream slices
         a.streams = S < a.npass ? S : a.npass;
+        // a workgroup stages the VLPs and sids of its own passes only (bdpt_kernels.hip nslot)
+        const size_t slots = ((size_t)a.npass + a.streams - 1) / a.streams;
+        const size_t smem = sizeof(float4) * (tab + 3 * slots + 5 + 4 * 128 * 2)
+                            + sizeof(unsigned) * (4 * 128 + slots + ids);
+        if (smem > 160 * 1024)
+            return fail(c, BDPT_EINVAL, "bdpt_path_passes: scene too large for LDS (%u spheres)", a.n);
         const void* kern = bdpt_path_kernel_table[(a.streams > 1) * 18 + kidx];
         const hipFunction_t jf = a.streams > 1 ? jf_streams : jf_fused;
         c->last_specialized = jf != nullptr;

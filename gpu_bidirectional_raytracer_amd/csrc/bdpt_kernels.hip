@@ -401,6 +401,13 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
 #endif
     const int ntree = kTreeLds ? 2 * a.bvh_nn + a.bvh_ns : 0;
     const int ntab = kBVH ? ntree + a.big_n : 4 * n;
+    // pass stream: this workgroup's lanes render passes s0, s0+S, s0+2S, ... (slots k = 0, 1, ...)
+    // of their pixels (S == 1: all, and each lane keeps the running mean itself; S > 1: radiance
+    // goes to rbuf, bdpt_accum_kernel folds it in pass order).  Only the slots' VLPs and sids are
+    // staged in LDS (one pass per workgroup with the default S = npass; bdpt_host.cpp sizes it).
+    const int S = STREAMS ? a.streams : 1, s0 = STREAMS ? (int)blockIdx.z : 0;
+    const int nslot = (a.npass - s0 + S - 1) / S;
+    const int mslot = (a.npass + S - 1) / S;         // slots of the LDS layout (any s0)
     float4* C = smem;                 // {cx, cy, cz, bits(refl | emissive<<8)}
     float4* E = smem + n;             // {ex, ey, ez, rad}
     float4* P = smem + 2 * n;         // {px, py, pz, 0}  (hit normal)
@@ -408,12 +415,12 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
     float4* ND = smem;                // BVH: nodes (2 float4 each)
     float4* SG = ND + 2 * a.bvh_nn;   // BVH: sphere geometry in leaf order
     float4* BG = smem + ntree;        // BVH: brute-force (wall) geometry
-    float4* V = smem + ntab;          // per pass: VLP {hx,hy,hz,rx}{ry,rz,nx,ny}{nz,-,-,-}
-    float4* K = V + 3 * a.npass;      // camera constants (5 float4)
+    float4* V = smem + ntab;          // per slot: VLP {hx,hy,hz,rx}{ry,rz,nx,ny}{nz,-,-,-}
+    float4* K = V + 3 * mslot;        // camera constants (5 float4)
     float4* Q = K + 5;                // shadow queues: 4 waves x kQueue x 2 float4
     unsigned* R = (unsigned*)(Q + 4 * kQueue * 2);    // shadow results: 4 x kQueue
-    unsigned* SID = R + 4 * kQueue;   // per pass sid
-    int* SI = (int*)(SID + a.npass);  // BVH: sphere ids (| emissive flag), leaf order
+    unsigned* SID = R + 4 * kQueue;   // per slot sid
+    int* SI = (int*)(SID + mslot);    // BVH: sphere ids (| emissive flag), leaf order
     int* BI = SI + (kTreeLds ? a.bvh_ns : 0);   // BVH: wall ids
     const float4* __restrict__ NDt = kTreeLds ? (const float4*)ND : a.bvh_nodes;
     const float4* __restrict__ SGt = kTreeLds ? (const float4*)SG : a.bvh_geom;
@@ -440,12 +447,13 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
             G[s] = make_float4(S.px, S.py, S.pz, S.rr);
         }
     }
-    for (int q = threadIdx.x; q < a.npass; q += 256) {
-        const bdpt_dev_lightpath L = a.lp[a.vlp[q] & (BDPT_DEV_LIGHT_POINTS - 1)];
+    for (int q = threadIdx.x; q < nslot; q += 256) {
+        const int pq = s0 + q * S;
+        const bdpt_dev_lightpath L = a.lp[a.vlp[pq] & (BDPT_DEV_LIGHT_POINTS - 1)];
         V[3 * q + 0] = make_float4(L.hx, L.hy, L.hz, L.rx);
         V[3 * q + 1] = make_float4(L.ry, L.rz, L.nx, L.ny);
         V[3 * q + 2] = make_float4(L.nz, 0.f, 0.f, 0.f);
-        SID[q] = a.sid[q];
+        SID[q] = a.sid[pq];
     }
     if (threadIdx.x == 0) {
         K[0] = make_float4(a.ux[0], a.ux[1], a.ux[2], a.tx);
@@ -489,10 +497,7 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
     const int y = ly + yoff;
     bool active = x < a.W && y < a.H;
     if (active && a.nshards > 1) active = ((y / a.band_rows) % a.nshards) == a.shard;
-    // pass stream: this lane renders passes s, s+S, s+2S, ... of its pixel (S == 1: all, and
-    // it keeps the running mean itself; S > 1: radiance goes to rbuf, bdpt_accum_kernel folds
-    // it in pass order).  Pass p is rendered iff counter0 + p < 30000 (one increment per pass).
-    const int S = STREAMS ? a.streams : 1, s0 = STREAMS ? (int)blockIdx.z : 0;
+    // Pass p = s0 + k*S (slot k) is rendered iff counter0 + p < 30000 (one increment per pass).
     float4* SQ = Q + wave * kQueue * 2;
     unsigned* SR = R + wave * kQueue;
 
@@ -516,13 +521,13 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
         cnt0 = a.counter[i];
     }
 
-    int p = s0;
+    int k = 0;                        // slot: this lane renders pass s0 + k*S next
     unsigned depth = 0;
-    unsigned j = (ibase + SID[p < a.npass ? p : 0]) % M5;
+    unsigned j = (ibase + SID[0]) % M5;
     float q0 = rnd[j], q1 = rnd[j + 1], q2 = rnd[j + 2], q3 = rnd[j + 3], q4 = rnd[j + 4];
     f3 ro = mk(0.f, 0.f, 0.f), rd = ro, thr = ro, rad = ro, nl = ro;
     bool specular = true, fresh = true;
-    bool alive = active && p < a.npass && cnt0 + (unsigned)p < BDPT_DEV_COUNTER_CAP;
+    bool alive = active && nslot > 0 && cnt0 + (unsigned)s0 < BDPT_DEV_COUNTER_CAP;
 
     while (__builtin_amdgcn_ballot_w64(alive) != 0) {                   // wave-uniform loop
 #ifdef BDPT_STATS
@@ -687,7 +692,7 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                     }
                 }
                 if (diff && li == 0) {                                    // the VLP (:507-537)
-                    const float4 v0 = V[3 * p], v1 = V[3 * p + 1], v2 = V[3 * p + 2];
+                    const float4 v0 = V[3 * k], v1 = V[3 * k + 1], v2 = V[3 * k + 2];
                     // a VLP with zero radiance adds exactly +0 to vres whether it is visible or
                     // not (wi * wo is finite): no ray.  Wave-uniform under pass streams, where a
                     // workgroup renders one pass (zero VLPs: cornell 6 %, cornell_glass 45 %)
@@ -826,7 +831,7 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
             if (!done && ++depth > 6) done = true;                       // :621 7-segment cap
             if (done) {                                                  // :774-787
                 if constexpr (!STREAMS) {
-                    const unsigned cnt = cnt0 + (unsigned)p;
+                    const unsigned cnt = cnt0 + (unsigned)k;      // S == 1: pass k
                     if (cnt == 0) {
                         col = rad;
                     } else {
@@ -842,12 +847,13 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                     unsigned xyv = xy;
                     asm volatile("" : "+v"(xyv));
                     const int li = ((int)(xyv >> 16) - yoff) * a.W + (int)(xyv & 0xffffu);
-                    a.rbuf[(size_t)p * a.nloc + (size_t)li] = r;
+                    a.rbuf[(size_t)(s0 + k * S) * a.nloc + (size_t)li] = r;
                 }
-                p += S;
+                k++;
                 fresh = true;
                 depth = 0;
-                alive = p < a.npass && cnt0 + (unsigned)p < BDPT_DEV_COUNTER_CAP;
+                const int pn = s0 + k * S;
+                alive = pn < a.npass && cnt0 + (unsigned)pn < BDPT_DEV_COUNTER_CAP;
             }
             if (alive) {                  // prefetch the next segment's random numbers (:619)
                 // 26 + 25 i and the pass's sid are rebuilt here rather than kept live across the
@@ -855,13 +861,13 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                 unsigned xyv = xy;
                 asm volatile("" : "+v"(xyv));
                 const unsigned li = (xyv >> 16) * (unsigned)a.W + (xyv & 0xffffu);
-                j = (26u + li * 25u + depth * 5u + SID[p]) % M5;
+                j = (26u + li * 25u + depth * 5u + SID[k]) % M5;
                 q0 = rnd[j]; q1 = rnd[j + 1]; q2 = rnd[j + 2]; q3 = rnd[j + 3]; q4 = rnd[j + 4];
             }
         }
     }
-    if (STREAMS || !active || p == s0) return;                           // nothing rendered
-    const unsigned cnt = cnt0 + (unsigned)p;
+    if (STREAMS || !active || k == 0) return;                            // nothing rendered
+    const unsigned cnt = cnt0 + (unsigned)k;
     bdpt_dev_vec out;
     out.x = col.x; out.y = col.y; out.z = col.z;
     a.colors[i] = out;

@@ -1,18 +1,19 @@
 #!/bin/bash
-# A/B of specialised-kernel compile options in one GPU session (BDPT_JIT_FLAGS; each flag set has
-# its own JIT cache entry).  Variants are separated by '|', "" = the default build:
-#   VARIANTS="|-DBDPT_SPLIT_TAIL=0" SCENES="cornell caustic" ROUNDS=2 bash scripts/ab_flags.sh
+# A/B of run-time settings in one GPU session: each variant is a list of VAR=VALUE environment
+# assignments (no spaces inside a value), variants separated by '|', "" = the default; e.g.
+# specialised-kernel compile options (BDPT_JIT_FLAGS; each option set has its own JIT cache entry):
+#   VARIANTS="|BDPT_JIT_FLAGS=-DBDPT_SPLIT_TAIL=0" SCENES="cornell caustic" ROUNDS=2 bash scripts/ab_flags.sh
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out; export TMPDIR=/tmp
 export BDPT_JIT_CACHE=$(mktemp -d /tmp/bdpt-jit-ab.XXXXXX)
-IFS='|' read -r -a VS <<< "${VARIANTS:-|-DBDPT_SPLIT_TAIL=0}"
+IFS='|' read -r -a VS <<< "${VARIANTS:-|BDPT_JIT_FLAGS=-DBDPT_SPLIT_TAIL=0}"
 for r in $(seq 1 ${ROUNDS:-2}); do
   for sc in ${SCENES:-cornell}; do
     k=0
     for v in "${VS[@]}"; do
       k=$((k+1))
-      BDPT_JIT_FLAGS="$v" timeout -k 10 300 python bench.py --no-cpu-baseline --scene $sc ${BENCH_ARGS:-} > gpurun_out/abf_$k.log 2>&1
+      env $v timeout -k 10 300 python bench.py --no-cpu-baseline --scene $sc ${BENCH_ARGS:-} > gpurun_out/abf_$k.log 2>&1
       rc=$?
       if [ $rc -ne 0 ]; then echo "STOP [$v] $sc rc=$rc"; tail -5 gpurun_out/abf_$k.log; exit $rc; fi
       echo "round $r $sc [${v:-default}] $(python -c "import json; d=json.loads(open('gpurun_out/abf_$k.log').read().strip().splitlines()[-1]); print(d['value'], d['device_ms_per_step'], d['config']['specialized'])")"
