@@ -50,6 +50,17 @@ extern "C" void bdpt_gamma_thresholds(float thr[256]);
 struct bdpt_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    // Pass-stream folds (bdpt_accum_kernel) run on their own stream so that a launch's fold
+    // overlaps the next launch's path kernel (VALU-bound; the fold is a memory stream).  The
+    // radiance buffer is double-buffered: launch L writes half L % 2 after the fold of launch L-2
+    // has read it.  Everything else that touches colors/counter/pixels runs on `stream` after
+    // join_fold() has made it wait for the last fold.
+    hipStream_t fstream = nullptr;
+    hipEvent_t rb_path_ev[2] = {nullptr, nullptr};   // path kernel of the half done (stream)
+    hipEvent_t rb_fold_ev[2] = {nullptr, nullptr};   // fold of the half done (fstream)
+    bool rb_used[2] = {false, false};
+    int rb_next = 0, fold_last = 0;
+    bool fold_pending = false;          // a fold was issued after the last join_fold
     // Path-pass calls go through a ring of kRing slots, each with its own pinned staging and
     // device copy of the pass tables (sid, vlp) and its own events, so a call never waits for
     // the GPU except on the call issued kRing calls earlier (the reference's interactive loop
@@ -79,7 +90,7 @@ struct bdpt_ctx {
     int last_streams = 1;               // S of the last path-pass launch
     bool last_bvh = false;              // the last path-pass launch traversed the BVH
     int cus = 256;                      // compute units (auto stream count)
-    bdpt_dev_vec* d_rbuf = nullptr;     // pass-stream radiance, [npass][nloc]
+    bdpt_dev_vec* d_rbuf = nullptr;     // pass-stream radiance, 2 halves of rbuf_cap: [npass][nloc]
     int traversal = BDPT_TRAVERSE_AUTO; // bdpt_set_traversal
     bool has_bvh = false;               // the scene has a BVH (bdpt_bvh.cpp)
     int bvh_nn = 0, bvh_ns = 0, big_n = 0;
@@ -250,6 +261,11 @@ static void release(bdpt_ctx* c) {
     }
     if (c->h_pass) (void)hipHostFree(c->h_pass);
     for (hipModule_t m : c->jit_mods) (void)hipModuleUnload(m);
+    for (int b = 0; b < 2; b++) {
+        if (c->rb_path_ev[b]) (void)hipEventDestroy(c->rb_path_ev[b]);
+        if (c->rb_fold_ev[b]) (void)hipEventDestroy(c->rb_fold_ev[b]);
+    }
+    if (c->fstream) (void)hipStreamDestroy(c->fstream);
     if (c->stream) (void)hipStreamDestroy(c->stream);
 }
 
@@ -506,6 +522,16 @@ static hipFunction_t jit_path_kernel(bdpt_ctx* c, bool streams) {
     }
 }
 
+// Make the context's stream wait for the last pass-stream fold (issued on fstream): call before
+// anything on `stream` touches colors/counter/pixels.  Folds run in order on fstream, so the last
+// one covers all.
+static int join_fold(bdpt_ctx* c) {
+    if (c->cpu || !c->fold_pending) return BDPT_OK;
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->rb_fold_ev[c->fold_last], 0));
+    c->fold_pending = false;
+    return BDPT_OK;
+}
+
 // Fold the calls issued before call number `upto` into the accumulators, oldest first (waits
 // for each of them to finish).
 static int fold_timing(bdpt_ctx* c, long long upto) {
@@ -575,6 +601,19 @@ int bdpt_create(bdpt_ctx** out, const bdpt_sphere* spheres, unsigned n, int W, i
     CK(hipSetDevice(device));
     CK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     {
+        // BDPT_FOLD_PRIORITY=high|low: the fold stream's priority (experiments; default normal)
+        const char* fp = getenv("BDPT_FOLD_PRIORITY");
+        int lo = 0, hi = 0;
+        if (fp && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess)
+            CK(hipStreamCreateWithPriority(&c->fstream, hipStreamNonBlocking, !strcmp(fp, "high") ? hi : lo));
+        else
+            CK(hipStreamCreateWithFlags(&c->fstream, hipStreamNonBlocking));
+    }
+    for (int b = 0; b < 2; b++) {
+        CK(hipEventCreateWithFlags(&c->rb_path_ev[b], hipEventDisableTiming));
+        CK(hipEventCreateWithFlags(&c->rb_fold_ev[b], hipEventDisableTiming));
+    }
+    {
         int cus = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
             c->cus = cus;
@@ -619,6 +658,7 @@ void bdpt_destroy(bdpt_ctx* c) {
     }
     destroy_group(c);
     (void)hipSetDevice(c->device);
+    if (c->fstream) (void)hipStreamSynchronize(c->fstream);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     release(c);
     delete c;
@@ -651,6 +691,7 @@ static int one_reset_accum(bdpt_ctx* c) {
         return BDPT_OK;
     }
     HIPCHK(c, hipSetDevice(c->device));
+    if (int rc = join_fold(c)) return rc;
     HIPCHK(c, hipMemsetAsync(c->d_counter, 0, sizeof(unsigned) * (size_t)c->W * c->H, c->stream));
     return BDPT_OK;
 }
@@ -856,6 +897,10 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
     int chunk = (int)((1L << 28) / per_pass);
     if (chunk < 1) chunk = 1;
     if (chunk > 128) chunk = 128;
+    if (const char* mp = getenv("BDPT_MAX_LAUNCH_PASSES")) {   // experiments: smaller launches
+        const int m = atoi(mp);
+        if (m >= 1 && m < chunk) chunk = m;
+    }
     if (S > chunk) S = chunk;
     if (S > npass) S = npass;
     if (S < 1) S = 1;
@@ -876,15 +921,16 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
         const int cmax = npass < chunk ? npass : chunk;
         const size_t need = (size_t)cmax * (size_t)lanes;
         if (need > c->rbuf_cap) {
-            HIPCHK(c, hipStreamSynchronize(c->stream));     // queued passes may use it
+            HIPCHK(c, hipStreamSynchronize(c->stream));     // queued passes and folds may use it
+            HIPCHK(c, hipStreamSynchronize(c->fstream));
             if (c->d_rbuf) HIPCHK(c, hipFree(c->d_rbuf));
             c->d_rbuf = nullptr;
             c->rbuf_cap = 0;
-            if (hipMalloc(&c->d_rbuf, sizeof(bdpt_dev_vec) * need) != hipSuccess)
-                return fail(c, BDPT_ENOMEM, "bdpt_path_passes: pass-stream buffer (%zu B)", sizeof(bdpt_dev_vec) * need);
+            c->rb_used[0] = c->rb_used[1] = false;
+            if (hipMalloc(&c->d_rbuf, 2 * sizeof(bdpt_dev_vec) * need) != hipSuccess)
+                return fail(c, BDPT_ENOMEM, "bdpt_path_passes: pass-stream buffer (2 x %zu B)", sizeof(bdpt_dev_vec) * need);
             c->rbuf_cap = need;
         }
-        a.rbuf = c->d_rbuf;
     }
     const size_t nchunks = grid_rows > 0 ? (size_t)((npass + chunk - 1) / chunk) : 0;
     while (cs.kev.size() < 2 * nchunks) {
@@ -930,6 +976,14 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
         c->last_specialized = jf != nullptr;
         void* kargs[] = {&a};
         grid.z = a.streams;
+        const int half = c->rb_next;
+        if (a.streams > 1) {
+            // this half was last read by the fold of the launch before the previous one
+            if (c->rb_used[half]) HIPCHK(c, hipStreamWaitEvent(c->stream, c->rb_fold_ev[half], 0));
+            a.rbuf = c->d_rbuf + (size_t)half * c->rbuf_cap;
+        } else if (int rc = join_fold(c)) {                  // the fused kernel updates colors itself
+            return rc;
+        }
         HIPCHK(c, hipEventRecord(cs.kev[2 * launches], c->stream));
         if (jf)
             HIPCHK(c, hipModuleLaunchKernel(jf, grid.x, grid.y, grid.z, block.x, 1, 1, (unsigned)smem,
@@ -937,12 +991,21 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
         else
             HIPCHK(c, hipLaunchKernel(kern, grid, block, kargs, smem, c->stream));
         HIPCHK(c, hipEventRecord(cs.kev[2 * launches + 1], c->stream));
-        if (a.streams > 1) {
+        if (a.streams > 1) {                                // the ordered fold, on fstream
             grid.z = 1;
-            HIPCHK(c, hipLaunchKernel((const void*)&bdpt_accum_kernel, grid, block, kargs, 0, c->stream));
+            HIPCHK(c, hipEventRecord(c->rb_path_ev[half], c->stream));
+            HIPCHK(c, hipStreamWaitEvent(c->fstream, c->rb_path_ev[half], 0));
+            HIPCHK(c, hipLaunchKernel((const void*)&bdpt_accum_kernel, grid, block, kargs, 0, c->fstream));
+            HIPCHK(c, hipEventRecord(c->rb_fold_ev[half], c->fstream));
+            c->rb_used[half] = true;
+            c->fold_last = half;
+            c->fold_pending = true;
+            c->rb_next = half ^ 1;
         }
     }
-    HIPCHK(c, hipEventRecord(cs.ev1, c->stream));
+    // the call ends with its last fold (fstream, which waited for the path kernels) if one is
+    // outstanding, else on the context's stream
+    HIPCHK(c, hipEventRecord(cs.ev1, c->fold_pending ? c->fstream : c->stream));
     cs.launches = launches;
     cs.pending = true;
     c->issued++;
@@ -953,6 +1016,7 @@ static int one_synchronize(bdpt_ctx* c) {
     if (!c) return BDPT_EINVAL;
     if (c->cpu) return BDPT_OK;
     HIPCHK(c, hipSetDevice(c->device));
+    if (int rc = join_fold(c)) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return fold_timing(c);
 }
@@ -990,6 +1054,7 @@ static int one_read_radiance(bdpt_ctx* c, bdpt_vec* colors, unsigned* counter) {
         return BDPT_OK;
     }
     HIPCHK(c, hipSetDevice(c->device));
+    if (int rc = join_fold(c)) return rc;
     const size_t np = (size_t)c->W * c->H;
     if (colors) HIPCHK(c, hipMemcpyAsync(colors, c->d_colors, sizeof(bdpt_vec) * np, hipMemcpyDeviceToHost, c->stream));
     if (counter) HIPCHK(c, hipMemcpyAsync(counter, c->d_counter, sizeof(unsigned) * np, hipMemcpyDeviceToHost, c->stream));
@@ -1004,6 +1069,7 @@ static int one_read_pixels(bdpt_ctx* c, unsigned char* rgba) {
         return BDPT_OK;
     }
     HIPCHK(c, hipSetDevice(c->device));
+    if (int rc = join_fold(c)) return rc;
     HIPCHK(c, hipMemcpyAsync(rgba, c->d_pixels, 4 * (size_t)c->W * c->H, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return BDPT_OK;
@@ -1037,6 +1103,8 @@ int bdpt_read_lightpaths(bdpt_ctx* c, bdpt_lightpath* lp) {
 static int one_device_buffers(bdpt_ctx* c, void** colors, void** counter, void** pixels) {
     if (!c) return BDPT_EINVAL;
     if (c->cpu) return fail(c, BDPT_EINVAL, "bdpt_device_buffers: the CPU backend has no device buffers");
+    HIPCHK(c, hipSetDevice(c->device));
+    if (int rc = join_fold(c)) return rc;                   // work queued on the stream follows the fold
     if (colors) *colors = c->d_colors;
     if (counter) *counter = c->d_counter;
     if (pixels) *pixels = c->d_pixels;
@@ -1050,6 +1118,7 @@ static int one_update_pixels(bdpt_ctx* c) {
         return BDPT_OK;
     }
     HIPCHK(c, hipSetDevice(c->device));
+    if (int rc = join_fold(c)) return rc;
     const int np = c->W * c->H;
     hipLaunchKernelGGL(bdpt_pixels_kernel, dim3((np + 255) / 256), dim3(256), 0, c->stream,
                        (const bdpt_dev_vec*)c->d_colors, c->d_pixels, (const float*)c->d_thr, np);
@@ -1105,6 +1174,7 @@ static void destroy_group(bdpt_ctx* c) {
     if (!c->multi) return;
     for (bdpt_ctx* p : c->peers) {
         (void)hipSetDevice(p->device);
+        if (p->fstream) (void)hipStreamSynchronize(p->fstream);
         if (p->stream) (void)hipStreamSynchronize(p->stream);
     }
     if (!c->comms.empty() && rccl().ok)
@@ -1377,6 +1447,7 @@ static int one_write_radiance(bdpt_ctx* c, const bdpt_vec* colors, const unsigne
         return BDPT_OK;
     }
     HIPCHK(c, hipSetDevice(c->device));
+    if (int rc = join_fold(c)) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     const size_t np = (size_t)c->W * c->H;
     std::vector<bdpt_vec> col;
