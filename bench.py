@@ -155,7 +155,7 @@ def main():
     ap.add_argument("--band-rows", type=int, default=None)
     ap.add_argument("--traversal", default="auto", choices=["auto", "brute", "bvh"],
                     help="sphere traversal for >16-sphere scenes (results identical)")
-    ap.add_argument("--streams", type=int, default=0, help="pass streams per pixel (0 = auto)")
+    ap.add_argument("--streams", type=int, default=0, help="pass streams per pixel (0 = auto: measured choice of one pass per lane or the fused kernel; -1 = one pass per lane; 1 = fused)")
     ap.add_argument("--specialize", type=int, default=1, choices=[0, 1],
                     help="scene-specialised kernels (run-time compiled; results identical)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)

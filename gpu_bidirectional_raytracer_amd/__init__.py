@@ -216,7 +216,7 @@ class Renderer:
         self._chk(lib.bdpt_set_shard(self._h, shard, nshards, band_rows))
 
     def set_streams(self, streams: int) -> None:
-        """Pass streams per pixel (0 = auto); results are bit-identical for every value."""
+        """Pass streams per pixel (0 = auto: measured choice, -1 = one pass per lane, 1 = fused); results are bit-identical for every value."""
         self._chk(lib.bdpt_set_streams(self._h, streams))
 
     @property

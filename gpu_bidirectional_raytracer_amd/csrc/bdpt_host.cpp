@@ -86,7 +86,17 @@ struct bdpt_ctx {
     bool cam_set = false;
     bool rand_ready = false;
     int shard = 0, nshards = 1, band_rows = 8;
-    int streams_req = 0;                // bdpt_set_streams: 0 = auto
+    int streams_req = 0;                // bdpt_set_streams: 0 = auto (measured), -1 = one pass per lane
+    // auto mode: the first two calls of >= 2 passes run the pass-stream kernels (one pass per lane)
+    // and the fused S = 1 kernel; their device times per pass decide for the later calls
+    // (tune_phase 0, 1: measuring; 2: both issued; 3: decided).  Reset by scene / shard /
+    // traversal / specialisation / stream-mode changes.  BDPT_STREAMS_TUNE=0: no measurement.
+    bool tune_enabled = true;
+    int tune_phase = 0;
+    bool tune_fused = false;
+    long long tune_call[2] = {-1, -1};
+    double tune_ms[2] = {0.0, 0.0};
+    int tune_npass[2] = {0, 0};
     int last_streams = 1;               // S of the last path-pass launch
     bool last_bvh = false;              // the last path-pass launch traversed the BVH
     int cus = 256;                      // compute units (auto stream count)
@@ -156,6 +166,7 @@ static int fail(bdpt_ctx* c, int code, const char* fmt, ...) {
     } while (0)
 
 static int upload_scene(bdpt_ctx* c) {
+    c->tune_phase = 0;                                      // re-measure the stream mode
     const unsigned n = (unsigned)c->spheres.size();
     // queued path passes may still read the scene buffers freed / rewritten below
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -543,6 +554,8 @@ static int fold_timing(bdpt_ctx* c, long long upto) {
         HIPCHK(c, hipEventElapsedTime(&ms, s.ev0, s.ev1));
         c->last_ms = ms;
         c->acc_ms += ms;
+        for (int r = 0; r < 2; r++)
+            if (c->folded == c->tune_call[r]) c->tune_ms[r] = ms;
         for (int k = 0; k < s.launches; k++) {
             float km = 0.f;
             HIPCHK(c, hipEventElapsedTime(&km, s.kev[2 * k], s.kev[2 * k + 1]));
@@ -600,6 +613,7 @@ int bdpt_create(bdpt_ctx** out, const bdpt_sphere* spheres, unsigned n, int W, i
         fail(c, BDPT_EHIP, "%s: %s", #call, hipGetErrorString(e_)); return bail(BDPT_EHIP); } } while (0)
     CK(hipSetDevice(device));
     CK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    if (const char* tv = getenv("BDPT_STREAMS_TUNE")) c->tune_enabled = atoi(tv) != 0;
     {
         // BDPT_FOLD_PRIORITY=high|low: the fold stream's priority (experiments; default normal)
         const char* fp = getenv("BDPT_FOLD_PRIORITY");
@@ -701,15 +715,17 @@ static int one_set_shard(bdpt_ctx* c, int shard, int nshards, int band_rows) {
         return c ? fail(c, BDPT_EINVAL, "bdpt_set_shard: bad shard %d/%d band %d", shard, nshards, band_rows)
                  : BDPT_EINVAL;
     c->shard = shard; c->nshards = nshards; c->band_rows = band_rows;
+    c->tune_phase = 0;
     if (c->cpu) bdpt_cpu_set_shard(c->cpu, shard, nshards, band_rows);
     return BDPT_OK;
 }
 
 static int one_set_streams(bdpt_ctx* c, int streams) {
     if (!c) return BDPT_EINVAL;
-    if (streams < 0 || streams > BDPT_MAX_STREAMS)
+    if (streams < BDPT_STREAMS_PER_LANE || streams > BDPT_MAX_STREAMS)
         return fail(c, BDPT_EINVAL, "bdpt_set_streams: bad stream count %d", streams);
     c->streams_req = streams;
+    c->tune_phase = 0;
     return BDPT_OK;
 }
 
@@ -718,6 +734,7 @@ int bdpt_last_streams(const bdpt_ctx* c) { return c ? c->last_streams : BDPT_EIN
 static int one_set_specialize(bdpt_ctx* c, int on) {
     if (!c) return BDPT_EINVAL;
     c->specialize = on != 0;
+    c->tune_phase = 0;
     return BDPT_OK;
 }
 
@@ -730,6 +747,7 @@ static int one_set_traversal(bdpt_ctx* c, int mode) {
     if (mode != BDPT_TRAVERSE_AUTO && mode != BDPT_TRAVERSE_BRUTE && mode != BDPT_TRAVERSE_BVH)
         return fail(c, BDPT_EINVAL, "bdpt_set_traversal: bad mode %d", mode);
     c->traversal = mode;
+    c->tune_phase = 0;
     return BDPT_OK;
 }
 
@@ -889,7 +907,22 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
     // sum (+11.7 % at 1080p, and it fills the GPU when a shard has few pixels).
     const long lanes = (long)grid_rows * BDPT_BTH * c->W;
     int S = c->streams_req;
-    if (S == 0) S = BDPT_MAX_STREAMS;
+    if (S <= 0) S = BDPT_MAX_STREAMS;
+    // auto: measure both kernels on the first two calls, then keep the faster
+    int tune_role = -1;
+    if (c->streams_req == 0 && c->tune_enabled) {
+        if (c->tune_phase == 2) {                            // waits for the second measured call
+            if (int rc = fold_timing(c, c->tune_call[1] + 1)) return rc;
+            c->tune_fused = c->tune_ms[1] * c->tune_npass[0] < c->tune_ms[0] * c->tune_npass[1];
+            c->tune_phase = 3;
+        }
+        if (c->tune_phase < 2 && npass >= 2) {
+            tune_role = c->tune_phase;
+            if (tune_role == 1) S = 1;
+        } else if (c->tune_phase == 3 && c->tune_fused) {
+            S = 1;
+        }
+    }
     a.nloc = (int)lanes;
     dim3 grid((c->W + BDPT_BTW - 1) / BDPT_BTW, grid_rows, 1), block(256);
     // keep single launches bounded (~2^28 samples, <= 128 passes for the LDS pass tables)
@@ -1008,6 +1041,11 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
     HIPCHK(c, hipEventRecord(cs.ev1, c->fold_pending ? c->fstream : c->stream));
     cs.launches = launches;
     cs.pending = true;
+    if (tune_role >= 0) {
+        c->tune_call[tune_role] = c->issued;
+        c->tune_npass[tune_role] = npass;
+        c->tune_phase = tune_role + 1;
+    }
     c->issued++;
     return BDPT_OK;
 }

@@ -174,9 +174,10 @@ def test_pass_streams_bit_exact(gpu, rnd0, streams):
     r.close()
 
 
-def test_auto_streams_policy(gpu):
-    """Auto: one pass per lane (S = passes in the launch, <= 128); 1 forces the fused kernel."""
+def test_per_lane_streams_policy(gpu):
+    """-1: one pass per lane (S = passes in the launch, <= 128); 1 forces the fused kernel."""
     r, _, _ = make("cornell", 1921, 1081, gpu)
+    r.set_streams(-1)
     sid, vlp = schedule(200)
     r.path_passes(sid[:1], vlp[:1])
     assert r.last_streams == 1
@@ -192,9 +193,41 @@ def test_auto_streams_policy(gpu):
     assert r.last_streams == 1
     r.close()
     s, _, _ = make("cornell", 65, 49, gpu)
+    s.set_streams(-1)
     s.path_passes(sid[:8], vlp[:8])
     assert s.last_streams == 8
     s.close()
+
+
+@pytest.mark.parametrize("name", ["cornell", "caustic"])
+def test_auto_streams_measured(gpu, rnd0, name):
+    """Auto (0): the first two calls of >= 2 passes run one pass per lane and the fused kernel,
+    later calls the one that measured faster; a scene change measures again.  Every call's
+    result is the oracle's whatever was chosen."""
+    W, H = 97, 65
+    r, cam, sp = make(name, W, H, gpu)
+    sid, vlp = schedule(40)
+    r.path_passes(sid[:1], vlp[:1])                        # 1 pass: not a measurement
+    assert r.last_streams == 1
+    r.path_passes(sid[1:9], vlp[1:9])
+    assert r.last_streams == 8                             # measures pass streams
+    r.path_passes(sid[9:17], vlp[9:17])
+    assert r.last_streams == 1                             # measures the fused kernel
+    used = []
+    for a0 in (17, 25):
+        r.path_passes(sid[a0:a0 + 8], vlp[a0:a0 + 8])
+        used.append(r.last_streams)
+    assert used[0] == used[1] and used[0] in (1, 8), used
+    col, cnt = r.read_radiance()
+    lp = oracle.light_pass(sp, rnd0, 0)
+    ocol, ocnt, opix = oracle.path_passes(sp, rnd0, cam, W, H, lp, sid[:33], vlp[:33])
+    assert_same(cnt, ocnt, "counter")
+    assert_same(col, ocol, "colors")
+    assert_same(r.read_pixels(), opix, "pixels")
+    r.set_scene(sp)                                        # ReInitScene: measure again
+    r.path_passes(sid[33:40], vlp[33:40])
+    assert r.last_streams == 7
+    r.close()
 
 
 def test_reset_accum_and_scene_edit(gpu, rnd0):
