@@ -963,6 +963,9 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
             if (hipMalloc(&c->d_rbuf, 2 * sizeof(bdpt_dev_vec) * need) != hipSuccess)
                 return fail(c, BDPT_ENOMEM, "bdpt_path_passes: pass-stream buffer (2 x %zu B)", sizeof(bdpt_dev_vec) * need);
             c->rbuf_cap = need;
+            // touch every page now (queued before this call's timing event): the first launch
+            // would otherwise pay the first-touch cost, and the stream-mode measurement with it
+            HIPCHK(c, hipMemsetAsync(c->d_rbuf, 0, 2 * sizeof(bdpt_dev_vec) * need, c->stream));
         }
     }
     const size_t nchunks = grid_rows > 0 ? (size_t)((npass + chunk - 1) / chunk) : 0;
