@@ -87,16 +87,19 @@ struct bdpt_ctx {
     bool rand_ready = false;
     int shard = 0, nshards = 1, band_rows = 8;
     int streams_req = 0;                // bdpt_set_streams: 0 = auto (measured), -1 = one pass per lane
-    // auto mode: the first two calls of >= 2 passes run the pass-stream kernels (one pass per lane)
-    // and the fused S = 1 kernel; their device times per pass decide for the later calls
-    // (tune_phase 0, 1: measuring; 2: both issued; 3: decided).  Reset by scene / shard /
+    // auto mode: the first three calls of >= 2 passes run the pass-stream kernels (one pass per
+    // lane), the fused S = 1 kernel, and the pass-stream kernels again; the fused kernel is kept
+    // only if its device time per pass beats the faster of the two pass-stream calls by
+    // kTuneMargin (a cold first call -- clocks still ramping -- no longer decides for the fused
+    // kernel).  tune_phase 0..2: measuring; 3: all issued; 4: decided.  Reset by scene / shard /
     // traversal / specialisation / stream-mode changes.  BDPT_STREAMS_TUNE=0: no measurement.
+    static constexpr double kTuneMargin = 0.02;
     bool tune_enabled = true;
     int tune_phase = 0;
     bool tune_fused = false;
-    long long tune_call[2] = {-1, -1};
-    double tune_ms[2] = {0.0, 0.0};
-    int tune_npass[2] = {0, 0};
+    long long tune_call[3] = {-1, -1, -1};
+    double tune_ms[3] = {0.0, 0.0, 0.0};
+    int tune_npass[3] = {0, 0, 0};
     int last_streams = 1;               // S of the last path-pass launch
     bool last_bvh = false;              // the last path-pass launch traversed the BVH
     int cus = 256;                      // compute units (auto stream count)
@@ -495,6 +498,20 @@ static hipFunction_t jit_path_kernel(bdpt_ctx* c, bool streams) {
         geom += (i ? ",{" : "{") + hexf(sp.p.x) + "," + hexf(sp.p.y) + "," + hexf(sp.p.z) + "," + hexf(rr) + "}";
     }
     geom += "}";
+    // the emitters' NEE records, formed exactly as upload_scene forms d_lightrec
+    std::string lrec = "{";
+    int nl = 0;
+    for (unsigned i = 0; i < n; i++) {
+        const bdpt_sphere& sp = c->spheres[i];
+        if (sp.e.x == 0.f && sp.e.y == 0.f && sp.e.z == 0.f) continue;
+        const float kPi = 3.14159265358979323846f;
+        const float area = 4.f * kPi * sp.rad * sp.rad;
+        lrec += std::string(nl ? "," : "") + "{" + hexf(sp.p.x) + "," + hexf(sp.p.y) + "," + hexf(sp.p.z) + "," +
+                hexf(sp.rad) + "},{" + hexf(sp.e.x) + "," + hexf(sp.e.y) + "," + hexf(sp.e.z) + "," + hexf(area) + "}";
+        nl++;
+    }
+    if (nl == 0) lrec += "{0,0,0,0},{0,0,0,0}";
+    lrec += "}";
     const char* wenv = getenv("BDPT_JIT_WAVES");
     int waves = wenv ? atoi(wenv) : 6;
     const std::string name = "&bdpt_path_kernel_t<" + std::to_string(n) + (streams ? ", true>" : ", false>");
@@ -503,12 +520,13 @@ static hipFunction_t jit_path_kernel(bdpt_ctx* c, bool streams) {
             "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize",
             "-fno-gpu-flush-denormals-to-zero", "-DBDPT_JIT=1", "-DBDPT_JIT_N=" + std::to_string(n),
             "-DBDPT_JIT_EMIS=" + std::to_string(emis) + "ull", "-DBDPT_JIT_GEOM=" + geom,
+            "-DBDPT_JIT_NL=" + std::to_string(nl), "-DBDPT_JIT_LREC=" + lrec,
             "-DBDPT_WAVES_PER_SIMD=" + std::to_string(waves)};
         std::vector<std::string> all = opts;
         if (const char* extra = getenv("BDPT_JIT_FLAGS")) {    // experiments: extra -D options
             std::string tok;
             for (const char* q = extra;; q++) {
-                if (*q == ' ' || *q == 0) {
+                if (*q == ' ' || *q == ',' || *q == 0) {
                     if (!tok.empty()) all.push_back(tok);
                     tok.clear();
                     if (!*q) break;
@@ -554,7 +572,7 @@ static int fold_timing(bdpt_ctx* c, long long upto) {
         HIPCHK(c, hipEventElapsedTime(&ms, s.ev0, s.ev1));
         c->last_ms = ms;
         c->acc_ms += ms;
-        for (int r = 0; r < 2; r++)
+        for (int r = 0; r < 3; r++)
             if (c->folded == c->tune_call[r]) c->tune_ms[r] = ms;
         for (int k = 0; k < s.launches; k++) {
             float km = 0.f;
@@ -911,15 +929,17 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
     // auto: measure both kernels on the first two calls, then keep the faster
     int tune_role = -1;
     if (c->streams_req == 0 && c->tune_enabled) {
-        if (c->tune_phase == 2) {                            // waits for the second measured call
-            if (int rc = fold_timing(c, c->tune_call[1] + 1)) return rc;
-            c->tune_fused = c->tune_ms[1] * c->tune_npass[0] < c->tune_ms[0] * c->tune_npass[1];
-            c->tune_phase = 3;
+        if (c->tune_phase == 3) {                            // waits for the last measured call
+            if (int rc = fold_timing(c, c->tune_call[2] + 1)) return rc;
+            const double a0 = c->tune_ms[0] / c->tune_npass[0], a2 = c->tune_ms[2] / c->tune_npass[2];
+            const double fused = c->tune_ms[1] / c->tune_npass[1];
+            c->tune_fused = fused * (1.0 + bdpt_ctx::kTuneMargin) < (a0 < a2 ? a0 : a2);
+            c->tune_phase = 4;
         }
-        if (c->tune_phase < 2 && npass >= 2) {
+        if (c->tune_phase < 3 && npass >= 2) {
             tune_role = c->tune_phase;
             if (tune_role == 1) S = 1;
-        } else if (c->tune_phase == 3 && c->tune_fused) {
+        } else if (c->tune_phase == 4 && c->tune_fused) {
             S = 1;
         }
     }
@@ -996,7 +1016,7 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
         a.vlp = d_vlp + p0;
         a.npass = npass - p0 < chunk ? npass - p0 : chunk;
         // scene tables (4 per sphere, or the BVH: 2 per node + 1 per sphere) + per-pass VLPs +
-        // camera + 4 wave shadow queues + results + sids (+ BVH sphere ids)
+        // camera + 4 wave shadow queues (results written over maxt) + sids (+ BVH sphere ids)
 #ifdef BDPT_BVH_LDS
         const size_t tree = 2 * (size_t)a.bvh_nn + a.bvh_ns, tree_ids = a.bvh_ns;
 #else
@@ -1008,8 +1028,10 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
         a.streams = S < a.npass ? S : a.npass;
         // a workgroup stages the VLPs and sids of its own passes only (bdpt_kernels.hip nslot)
         const size_t slots = ((size_t)a.npass + a.streams - 1) / a.streams;
-        const size_t smem = sizeof(float4) * (tab + 3 * slots + 5 + 4 * 128 * 2)
-                            + sizeof(unsigned) * (4 * 128 + slots + ids);
+        size_t smem = sizeof(float4) * (tab + 3 * slots + 5 + 4 * 128 * 2)
+                      + sizeof(unsigned) * (slots + ids);
+        if (const char* pad = getenv("BDPT_SMEM_PAD"))       // experiments: cap workgroups per CU
+            smem += (size_t)atoi(pad);
         if (smem > 160 * 1024)
             return fail(c, BDPT_EINVAL, "bdpt_path_passes: scene too large for LDS (%u spheres)", a.n);
         const void* kern = bdpt_path_kernel_table[(a.streams > 1) * 18 + kidx];

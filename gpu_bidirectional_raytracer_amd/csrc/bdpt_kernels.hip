@@ -23,6 +23,15 @@
 struct jit_geom { float x, y, z, w; };
 constexpr jit_geom kJitGeom[BDPT_JIT_N] = BDPT_JIT_GEOM;
 constexpr unsigned long long kJitEmis = BDPT_JIT_EMIS;
+// the emitters' NEE records {p, rad}, {e, (4*pi*rad)*rad} (bdpt_host.cpp upload_scene), folded too
+// Folding the NEE records too (BDPT_JIT_LIGHTS=1) frees 8 VGPRs (71: 7 waves/SIMD, 64 without
+// spills at 8) but the compiler then issues 2.5 % more VALU instructions, and every occupancy from
+// 5 to 8 waves/SIMD measured the same: cornell -1 to -2 %, so it is off by default.
+#ifndef BDPT_JIT_LIGHTS
+#define BDPT_JIT_LIGHTS 0
+#endif
+constexpr int kJitNL = BDPT_JIT_NL;
+constexpr jit_geom kJitLrec[2 * (BDPT_JIT_NL > 0 ? BDPT_JIT_NL : 1)] = BDPT_JIT_LREC;
 #endif
 
 namespace {
@@ -51,11 +60,30 @@ __device__ __forceinline__ float rcp_rn(float x) {
     if (__builtin_expect(!(ax >= 0x1p-125f && ax < 0x1p125f), 0)) return 1.f / x;
     return rcp_rn_inrange(x);
 }
+// 1.f / sqrtf(x) with both operations correctly rounded, one range test for the pair: for x in
+// [2^-96, 2^126) the fast sqrt is exact and its root lies in [2^-48, 2^63), inside rcp_rn's range.
+__device__ __forceinline__ float rcp_sqrt_rn(float x, float* root) {
+    if (__builtin_expect(!(x >= 0x1p-96f && x < 0x1p126f), 0)) {
+        *root = sqrtf(x);
+        return 1.f / *root;
+    }
+    *root = bdpt_sqrt_rn_core(x);
+    return rcp_rn_inrange(*root);
+}
+
+#ifndef BDPT_NORM1
+#define BDPT_NORM1 1
+#endif
 __device__ __forceinline__ f3 norm(f3 v) {
 #ifdef BDPT_ABL_DIV
     return smul(__builtin_amdgcn_rsqf(dot(v, v)), v);
 #endif
+#if BDPT_NORM1
+    float root;
+    return smul(rcp_sqrt_rn(dot(v, v), &root), v);             // one range test (above)
+#else
     float l = rcp_rn(bdpt_sqrt_rn(dot(v, v))); return smul(l, v);
+#endif
 }
 __device__ __forceinline__ f3 cross(f3 a, f3 b) {
     return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
@@ -121,6 +149,48 @@ __device__ __forceinline__ float sphere_isect_inf(float4 g, f3 o, f3 d) {
     const float t1 = b - s, t2 = b + s;
     const float r = t1 > kEps ? t1 : t2;
     return r > kEps ? r : __builtin_inff();
+}
+
+// Hit distances as unsigned keys (path kernel; brute-force traversal): key(x) = bits(x) - kKeyC
+// mod 2^32 with kKeyC = bits(EPSILON) + 1.  For x > EPSILON (+inf included) key(x) <= key(+inf) =
+// 0x435C28F5 and the key increases with x; every x <= EPSILON (+0 included), every NaN and every
+// negative float maps above that (the subtraction wraps, or the sign bit survives it).  t1 <= t2
+// (fl is monotone and the root is >= 0, or both are NaN), so min(key(t1), key(t2)) is
+// key(t1 > EPS ? t1 : t2) when that value is > EPS, and a key above key(+inf) -- a miss --
+// otherwise: the closest-hit update `d != 0 && d < t` of device.cu:106-124 becomes one unsigned
+// min3 with the running key, and the shadow test EPS < r < maxt one unsigned compare against
+// key(maxt) (0 when maxt <= EPS or NaN: no sphere can occlude, as in the float test).
+// Measured slower, so off by default (BDPT_IKEY=1 builds it): with the keys the path kernel issues
+// 2 % fewer VALU instructions on cornell but runs 1-2 % longer (A/B in one session):
+// the saved compares and selects were replaced by integer min/min3, which gfx950 issues at half
+// the rate of fp32 add/mul/fma (scripts/valu_rates.hip).
+#ifndef BDPT_IKEY
+#define BDPT_IKEY 0
+#endif
+constexpr unsigned kKeyC = 0x3C23D70Bu;                      // bits(0.01f) + 1
+struct tkeys { unsigned k1, k2; };
+__device__ __forceinline__ tkeys sphere_keys(float4 g, f3 o, f3 d) {
+    f3 op = mk(g.x - o.x, g.y - o.y, g.z - o.z);
+    float b = dot(op, d);
+    float det = b * b - dot(op, op) + g.w;
+    const float s = bdpt_sqrt_rn_core(det);
+    const float t1 = b - s, t2 = b + s;
+    return {__float_as_uint(t1) - kKeyC, __float_as_uint(t2) - kKeyC};
+}
+__device__ __forceinline__ unsigned umin(unsigned a, unsigned b) { return a < b ? a : b; }
+// min(a, b, c) as one v_min3_u32: written out because the compiler, seeing `min3 < a`, compares
+// min(b, c) with a instead and then keeps min(b, c) for a separate v_min_u32
+__device__ __forceinline__ unsigned umin3(unsigned a, unsigned b, unsigned c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    unsigned r;
+    asm("v_min3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+#else
+    return umin(a, umin(b, c));
+#endif
+}
+__device__ __forceinline__ unsigned maxt_key(float maxt) {
+    return maxt > kEps ? __float_as_uint(maxt) - kKeyC : 0u;
 }
 
 // UniformSampleSphereDevice device.cu:157-165
@@ -418,8 +488,8 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
     float4* V = smem + ntab;          // per slot: VLP {hx,hy,hz,rx}{ry,rz,nx,ny}{nz,-,-,-}
     float4* K = V + 3 * mslot;        // camera constants (5 float4)
     float4* Q = K + 5;                // shadow queues: 4 waves x kQueue x 2 float4
-    unsigned* R = (unsigned*)(Q + 4 * kQueue * 2);    // shadow results: 4 x kQueue
-    unsigned* SID = R + 4 * kQueue;   // per slot sid
+    // (a ray's occlusion bit is written over its maxt, SQ[idx].w, once the ray is traced)
+    unsigned* SID = (unsigned*)(Q + 4 * kQueue * 2);   // per slot sid
     int* SI = (int*)(SID + mslot);    // BVH: sphere ids (| emissive flag), leaf order
     int* BI = SI + (kTreeLds ? a.bvh_ns : 0);   // BVH: wall ids
     const float4* __restrict__ NDt = kTreeLds ? (const float4*)ND : a.bvh_nodes;
@@ -499,7 +569,6 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
     if (active && a.nshards > 1) active = ((y / a.band_rows) % a.nshards) == a.shard;
     // Pass p = s0 + k*S (slot k) is rendered iff counter0 + p < 30000 (one increment per pass).
     float4* SQ = Q + wave * kQueue * 2;
-    unsigned* SR = R + wave * kQueue;
 
     const int i = active ? y * a.W + x : 0;
     const unsigned ibase = 26u + (unsigned)(i * 25);
@@ -597,11 +666,23 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                     }
                 }
             } else {
+#if BDPT_IKEY
+                unsigned kt = __float_as_uint(1e20f) - kKeyC;     // key(t), see sphere_keys
+#pragma unroll kUnroll
+                for (int s = n - 1; s >= 0; --s) {
+                    const tkeys k = sphere_keys(geom(s), ro, rd);
+                    const unsigned nk = umin3(kt, k.k1, k.k2);
+                    id = nk < kt ? s : id;
+                    kt = nk;
+                }
+                t = __uint_as_float(kt + kKeyC);
+#else
 #pragma unroll kUnroll
                 for (int s = n - 1; s >= 0; --s) {
                     const float d = sphere_isect_inf(geom(s), ro, rd);
                     if (d < t) { t = d; id = s; }
                 }
+#endif
             }
             done = id < 0;
             if (!done) {
@@ -668,18 +749,32 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
         if (__builtin_amdgcn_ballot_w64(diff) != 0) {
             f3 res = mk(0.f, 0.f, 0.f), usp = res, vsd = res, vcon = res;
             if (diff) usp = uniform_sphere<true>(q3, q4, SCT);
-            const int nsteps = a.n_lights > 0 ? (int)a.n_lights : 1;
+#if defined(BDPT_JIT) && BDPT_JIT_LIGHTS
+            const int nlights = N == BDPT_JIT_N ? kJitNL : (int)a.n_lights;
+#else
+            const int nlights = (int)a.n_lights;
+#endif
+            auto lrec = [&](int k) -> float4 {
+#if defined(BDPT_JIT) && BDPT_JIT_LIGHTS
+                if constexpr (N == BDPT_JIT_N) {
+                    const jit_geom g = kJitLrec[k];
+                    return make_float4(g.x, g.y, g.z, g.w);
+                }
+#endif
+                return ld_const(a.lightrec, k);
+            };
+            const int nsteps = nlights > 0 ? nlights : 1;
             for (int li = 0; li < nsteps; li++) {                         // uniform
                 bool has_nee = false, has_vlp = false;
                 f3 sd = res, con = res;
                 float maxt = 0.f, vmaxt = 0.f;
-                if (diff && a.n_lights > 0) {
-                    const float4 lg = ld_const(a.lightrec, 2 * li);       // {p, rad}
-                    const float4 le = ld_const(a.lightrec, 2 * li + 1);   // {e, 4*pi*rad*rad}
+                if (diff && nlights > 0) {
+                    const float4 lg = lrec(2 * li);                       // {p, rad}
+                    const float4 le = lrec(2 * li + 1);                   // {e, 4*pi*rad*rad}
                     const f3 spt = add(smul(lg.w, usp), mk(lg.x, lg.y, lg.z));
                     sd = sub(spt, ro);
-                    const float len = bdpt_sqrt_rn(dot(sd, sd));
-                    sd = smul(rcp_rn(len), sd);
+                    float len;
+                    sd = smul(rcp_sqrt_rn(dot(sd, sd), &len), sd);
                     float wo = dot(sd, usp);
                     if (!(wo > 0.f)) {
                         wo = -wo;
@@ -698,8 +793,8 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                     // workgroup renders one pass (zero VLPs: cornell 6 %, cornell_glass 45 %)
                     if (!(v0.w == 0.f && v1.x == 0.f && v1.y == 0.f)) {
                         vsd = sub(mk(v0.x, v0.y, v0.z), ro);
-                        const float len = bdpt_sqrt_rn(dot(vsd, vsd));
-                        vsd = smul(rcp_rn(len), vsd);
+                        float len;
+                        vsd = smul(rcp_sqrt_rn(dot(vsd, vsd), &len), vsd);
                         float wo = dot(vsd, mk(v1.z, v1.w, v2.x));
                         if (!(wo > 0.f)) {
                             wo = -wo;
@@ -758,14 +853,22 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                                 const float4 r0 = SQ[base + r], r1 = SQ[kQueue + base + r];
                                 const f3 o = mk(r0.x, r0.y, r0.z), d = mk(r1.x, r1.y, r1.z);
                                 const bool vac = r1.w != 0.f;
+#if BDPT_IKEY
+                                const unsigned km = maxt_key(r0.w);
+                                for (int s = n - 1 - g; s >= 0; s -= 1 << lg) {
+                                    const tkeys k = sphere_keys(G[s], o, d);
+                                    if (umin(k.k1, k.k2) < km && !(vac && emissive(s))) { occ = 1; break; }
+                                }
+#else
                                 for (int s = n - 1 - g; s >= 0; s -= 1 << lg) {
                                     const float dd = sphere_isect_inf(G[s], o, d);
                                     if (dd < r0.w && !(vac && emissive(s))) { occ = 1; break; }
                                 }
+#endif
                             }
                             unsigned long long m = __builtin_amdgcn_ballot_w64(occ != 0);
                             for (int w = 32; w >= rpg; w >>= 1) m |= m >> w;   // uniform
-                            if (lane < c) SR[base + lane] = (unsigned)(m >> lane) & 1u;
+                            if (lane < c) SQ[base + lane].w = __uint_as_float((unsigned)(m >> lane) & 1u);
                             continue;
                         }
                     }
@@ -800,6 +903,14 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                                 node = occ ? a.bvh_nn : __float_as_int(lo.w);
                             }
                         } else {
+#if BDPT_IKEY
+                        const unsigned km = maxt_key(r0.w);
+#pragma unroll kUnroll
+                        for (int s = n - 1; s >= 0; --s) {                // IntersectP(Vacuum)Device
+                            const tkeys k = sphere_keys(geom(s), o, d);
+                            if (umin(k.k1, k.k2) < km && !(vac && emissive(s))) { occ = 1; break; }
+                        }
+#else
 #pragma unroll kUnroll
                         for (int s = n - 1; s >= 0; --s) {                // IntersectP(Vacuum)Device
                             const float dd = sphere_isect_inf(geom(s), o, d);
@@ -807,13 +918,14 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                             // branch-free running minimum of integer-keyed distances)
                             if (dd < r0.w && !(vac && emissive(s))) { occ = 1; break; }
                         }
+#endif
                         }
-                        SR[idx] = occ;
+                        SQ[idx].w = __uint_as_float(occ);
                     }
                 }
                 wave_lds_fence();
-                if (has_nee && SR[pn] == 0) res = add(res, con);
-                if (has_vlp && SR[pv] != 0) vcon = mk(0.f, 0.f, 0.f);
+                if (has_nee && __float_as_uint(SQ[pn].w) == 0) res = add(res, con);
+                if (has_vlp && __float_as_uint(SQ[pv].w) != 0) vcon = mk(0.f, 0.f, 0.f);
                 if (li == 0 && !has_vlp) vcon = mk(0.f, 0.f, 0.f);
                 wave_lds_fence();
             }

@@ -201,31 +201,34 @@ def test_per_lane_streams_policy(gpu):
 
 @pytest.mark.parametrize("name", ["cornell", "caustic"])
 def test_auto_streams_measured(gpu, rnd0, name):
-    """Auto (0): the first two calls of >= 2 passes run one pass per lane and the fused kernel,
-    later calls the one that measured faster; a scene change measures again.  Every call's
-    result is the oracle's whatever was chosen."""
+    """Auto (0): the first three calls of >= 2 passes run one pass per lane, the fused kernel
+    and one pass per lane again; later calls use the fused kernel only if it measured faster than
+    both pass-stream calls; a scene change measures again.  Every call's result is the oracle's
+    whatever was chosen."""
     W, H = 97, 65
     r, cam, sp = make(name, W, H, gpu)
-    sid, vlp = schedule(40)
+    sid, vlp = schedule(48)
     r.path_passes(sid[:1], vlp[:1])                        # 1 pass: not a measurement
     assert r.last_streams == 1
     r.path_passes(sid[1:9], vlp[1:9])
     assert r.last_streams == 8                             # measures pass streams
     r.path_passes(sid[9:17], vlp[9:17])
     assert r.last_streams == 1                             # measures the fused kernel
+    r.path_passes(sid[17:25], vlp[17:25])
+    assert r.last_streams == 8                             # pass streams again
     used = []
-    for a0 in (17, 25):
+    for a0 in (25, 33):
         r.path_passes(sid[a0:a0 + 8], vlp[a0:a0 + 8])
         used.append(r.last_streams)
     assert used[0] == used[1] and used[0] in (1, 8), used
     col, cnt = r.read_radiance()
     lp = oracle.light_pass(sp, rnd0, 0)
-    ocol, ocnt, opix = oracle.path_passes(sp, rnd0, cam, W, H, lp, sid[:33], vlp[:33])
+    ocol, ocnt, opix = oracle.path_passes(sp, rnd0, cam, W, H, lp, sid[:41], vlp[:41])
     assert_same(cnt, ocnt, "counter")
     assert_same(col, ocol, "colors")
     assert_same(r.read_pixels(), opix, "pixels")
     r.set_scene(sp)                                        # ReInitScene: measure again
-    r.path_passes(sid[33:40], vlp[33:40])
+    r.path_passes(sid[41:48], vlp[41:48])
     assert r.last_streams == 7
     r.close()
 
