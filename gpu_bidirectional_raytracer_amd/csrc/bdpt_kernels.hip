@@ -151,48 +151,6 @@ __device__ __forceinline__ float sphere_isect_inf(float4 g, f3 o, f3 d) {
     return r > kEps ? r : __builtin_inff();
 }
 
-// Hit distances as unsigned keys (path kernel; brute-force traversal): key(x) = bits(x) - kKeyC
-// mod 2^32 with kKeyC = bits(EPSILON) + 1.  For x > EPSILON (+inf included) key(x) <= key(+inf) =
-// 0x435C28F5 and the key increases with x; every x <= EPSILON (+0 included), every NaN and every
-// negative float maps above that (the subtraction wraps, or the sign bit survives it).  t1 <= t2
-// (fl is monotone and the root is >= 0, or both are NaN), so min(key(t1), key(t2)) is
-// key(t1 > EPS ? t1 : t2) when that value is > EPS, and a key above key(+inf) -- a miss --
-// otherwise: the closest-hit update `d != 0 && d < t` of device.cu:106-124 becomes one unsigned
-// min3 with the running key, and the shadow test EPS < r < maxt one unsigned compare against
-// key(maxt) (0 when maxt <= EPS or NaN: no sphere can occlude, as in the float test).
-// Measured slower, so off by default (BDPT_IKEY=1 builds it): with the keys the path kernel issues
-// 2 % fewer VALU instructions on cornell but runs 1-2 % longer (A/B in one session):
-// the saved compares and selects were replaced by integer min/min3, which gfx950 issues at half
-// the rate of fp32 add/mul/fma (scripts/valu_rates.hip).
-#ifndef BDPT_IKEY
-#define BDPT_IKEY 0
-#endif
-constexpr unsigned kKeyC = 0x3C23D70Bu;                      // bits(0.01f) + 1
-struct tkeys { unsigned k1, k2; };
-__device__ __forceinline__ tkeys sphere_keys(float4 g, f3 o, f3 d) {
-    f3 op = mk(g.x - o.x, g.y - o.y, g.z - o.z);
-    float b = dot(op, d);
-    float det = b * b - dot(op, op) + g.w;
-    const float s = bdpt_sqrt_rn_core(det);
-    const float t1 = b - s, t2 = b + s;
-    return {__float_as_uint(t1) - kKeyC, __float_as_uint(t2) - kKeyC};
-}
-__device__ __forceinline__ unsigned umin(unsigned a, unsigned b) { return a < b ? a : b; }
-// min(a, b, c) as one v_min3_u32: written out because the compiler, seeing `min3 < a`, compares
-// min(b, c) with a instead and then keeps min(b, c) for a separate v_min_u32
-__device__ __forceinline__ unsigned umin3(unsigned a, unsigned b, unsigned c) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    unsigned r;
-    asm("v_min3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-    return r;
-#else
-    return umin(a, umin(b, c));
-#endif
-}
-__device__ __forceinline__ unsigned maxt_key(float maxt) {
-    return maxt > kEps ? __float_as_uint(maxt) - kKeyC : 0u;
-}
-
 // UniformSampleSphereDevice device.cu:157-165
 template <bool TAB = false>
 __device__ __forceinline__ f3 uniform_sphere(float u1, float u2, const double* tab = nullptr) {
@@ -372,6 +330,14 @@ __device__ __forceinline__ float4 ld_const(const float4* p, int i) {
 #endif
 }
 
+// f(S), f(S-1), ..., f(0) with compile-time indices while f returns true
+template <int S, typename F>
+__device__ __forceinline__ void unroll_down(F& f) {
+    if constexpr (S >= 0) {
+        if (f(S)) unroll_down<S - 1>(f);
+    }
+}
+
 __device__ __forceinline__ void wave_lds_fence() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -444,6 +410,10 @@ extern "C" int bdpt_debug_stats(unsigned long long* out, int reset) {
 // Part-full shadow rounds split the sphere list over lane groups (path kernel, shadow queue).
 #ifndef BDPT_SPLIT_TAIL
 #define BDPT_SPLIT_TAIL 1
+#endif
+// Shadow rays of full rounds: occlusion kept as a wave lane mask with a uniform exit
+#ifndef BDPT_ANYHIT_MASK
+#define BDPT_ANYHIT_MASK 1
 #endif
 // (the specialised build is compiled with -DBDPT_WAVES_PER_SIMD=6: folding the scene in frees
 // registers, and 6 waves/SIMD measured +3 % over 5 on cornell)
@@ -666,23 +636,11 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                     }
                 }
             } else {
-#if BDPT_IKEY
-                unsigned kt = __float_as_uint(1e20f) - kKeyC;     // key(t), see sphere_keys
-#pragma unroll kUnroll
-                for (int s = n - 1; s >= 0; --s) {
-                    const tkeys k = sphere_keys(geom(s), ro, rd);
-                    const unsigned nk = umin3(kt, k.k1, k.k2);
-                    id = nk < kt ? s : id;
-                    kt = nk;
-                }
-                t = __uint_as_float(kt + kKeyC);
-#else
 #pragma unroll kUnroll
                 for (int s = n - 1; s >= 0; --s) {
                     const float d = sphere_isect_inf(geom(s), ro, rd);
                     if (d < t) { t = d; id = s; }
                 }
-#endif
             }
             done = id < 0;
             if (!done) {
@@ -853,18 +811,10 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                                 const float4 r0 = SQ[base + r], r1 = SQ[kQueue + base + r];
                                 const f3 o = mk(r0.x, r0.y, r0.z), d = mk(r1.x, r1.y, r1.z);
                                 const bool vac = r1.w != 0.f;
-#if BDPT_IKEY
-                                const unsigned km = maxt_key(r0.w);
-                                for (int s = n - 1 - g; s >= 0; s -= 1 << lg) {
-                                    const tkeys k = sphere_keys(G[s], o, d);
-                                    if (umin(k.k1, k.k2) < km && !(vac && emissive(s))) { occ = 1; break; }
-                                }
-#else
                                 for (int s = n - 1 - g; s >= 0; s -= 1 << lg) {
                                     const float dd = sphere_isect_inf(G[s], o, d);
                                     if (dd < r0.w && !(vac && emissive(s))) { occ = 1; break; }
                                 }
-#endif
                             }
                             unsigned long long m = __builtin_amdgcn_ballot_w64(occ != 0);
                             for (int w = 32; w >= rpg; w >>= 1) m |= m >> w;   // uniform
@@ -903,13 +853,27 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                                 node = occ ? a.bvh_nn : __float_as_int(lo.w);
                             }
                         } else {
-#if BDPT_IKEY
-                        const unsigned km = maxt_key(r0.w);
-#pragma unroll kUnroll
-                        for (int s = n - 1; s >= 0; --s) {                // IntersectP(Vacuum)Device
-                            const tkeys k = sphere_keys(geom(s), o, d);
-                            if (umin(k.k1, k.k2) < km && !(vac && emissive(s))) { occ = 1; break; }
-                        }
+#if BDPT_ANYHIT_MASK
+                        // occlusion as a wave lane mask (SGPRs): every lane tests every sphere
+                        // until all of the round's rays are occluded (one uniform branch per
+                        // sphere).  No per-lane break, so no nest of saved exec masks -- for 64
+                        // spheres those spilled to VGPR lanes -- and no per-sphere register copy
+                        // of the flag; a lane's further tests cannot change its OR.
+                        const unsigned long long live = __builtin_amdgcn_ballot_w64(true);
+                        const unsigned long long vacm = __builtin_amdgcn_ballot_w64(vac);
+                        unsigned long long occm = 0;
+                        auto step = [&](int s) -> bool {                  // IntersectP(Vacuum)Device
+                            const float dd = sphere_isect_inf(geom(s), o, d);
+                            unsigned long long h = __builtin_amdgcn_ballot_w64(dd < r0.w);
+                            if (emissive(s)) h &= ~vacm;
+                            occm |= h;
+                            return occm != live;
+                        };
+                        // spheres n-1 .. 0; unrolled by template recursion (the loop unroller
+                        // leaves a loop holding a ballot alone)
+                        if constexpr (N > 0) unroll_down<N - 1>(step);
+                        else for (int s = n - 1; s >= 0 && step(s); --s) {}
+                        occ = (unsigned)(occm >> lane) & 1u;
 #else
 #pragma unroll kUnroll
                         for (int s = n - 1; s >= 0; --s) {                // IntersectP(Vacuum)Device
