@@ -182,6 +182,27 @@ __device__ __forceinline__ f3 cosine_dir(f3 w, float u_phi, float u_r2, const do
     return add(nd, w);
 }
 
+// The rest of cosine_dir once u = normalize(cross(a, w)) and r2s = sqrt(r2) are known (the path
+// kernel computes those two on a path shared with refraction): the same operations in the same
+// order as cosine_dir.
+template <bool TAB = false>
+__device__ __forceinline__ f3 cosine_tail(f3 w, f3 u, float u_phi, float u_r2, float r2s,
+                                          const double* tab = nullptr) {
+    const float r1 = 2.f * kPi * u_phi;
+    f3 v = cross(w, u);
+    float s, c;
+    sincos_cr<TAB>(r1, &s, &c, tab);
+    u = smul(c * r2s, u);
+    v = smul(s * r2s, v);
+    f3 nd = add(u, v);
+    w = smul(bdpt_sqrt_rn_core(1 - u_r2), w);                // 1 - r2 is 0 or >= 2^-24
+    return add(nd, w);
+}
+
+#ifndef BDPT_MERGE_REFR
+#define BDPT_MERGE_REFR 1
+#endif
+
 }  // namespace
 
 #ifndef BDPT_JIT
@@ -657,6 +678,73 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                         rad = add(rad, mul(thr, smul(fabsf(dp), mk(em.x, em.y, em.z))));
                     }
                     done = true;
+#if BDPT_MERGE_REFR
+                } else {
+                    // DIFF (:663-703), SPEC (:704-714), REFR (:715-770).  Nearly every wave holds
+                    // a few refracting lanes next to its diffuse ones, so the diffuse and the
+                    // refraction code both run; their square root (sqrt(r2) | sqrt(cos2t)) and
+                    // their normalisation (u | the transmitted direction) are one shared
+                    // instruction sequence on lane-selected inputs -- the same float operations
+                    // per lane, so the results are unchanged.
+                    const bool isdiff = (mat & 255) == BDPT_DEV_DIFF;
+                    const f3 cc = mk(cm.x, cm.y, cm.z);
+                    f3 refl = rd;
+                    bool refr = false, into = false;
+                    float nnt = 0.f, ddn = 0.f, cos2t = 0.f;
+                    const float nc = 1.f, nt = 1.5f;
+                    if (!isdiff) {
+                        specular = true;
+                        refl = sub(rd, smul(2.f * dot(normal, rd), normal));
+                        if ((mat & 255) == BDPT_DEV_SPEC) {
+                            thr = mul(thr, cc);
+                            rd = refl;
+                        } else {
+                            into = dot(normal, nl) > 0;
+                            nnt = into ? nc / nt : nt / nc;
+                            ddn = dot(rd, nl);
+                            cos2t = 1.f - nnt * nnt * (1.f - ddn * ddn);
+                            if (cos2t < 0.f) {
+                                thr = mul(thr, cc);
+                                rd = refl;
+                            } else {
+                                refr = true;
+                            }
+                        }
+                    }
+                    if (isdiff || refr) {
+                        // r2 = d_Rand value >= 2^-32; cos2t = 1 - X is 0 or >= 2^-24: core exact
+                        const float s1 = bdpt_sqrt_rn_core(isdiff ? q1 : cos2t);
+                        f3 V;
+                        if (isdiff) {
+                            const f3 ax = fabsf(nl.x) > .1f ? mk(0.f, 1.f, 0.f) : mk(1.f, 0.f, 0.f);
+                            V = cross(ax, nl);                    // |V|^2 >= 0.01 by the choice
+                        } else {
+                            const float kq = (float)(into ? 1 : -1) * (ddn * nnt + s1);
+                            V = sub(smul(nnt, rd), smul(kq, normal));
+                        }
+                        float root;
+                        const f3 U = smul(rcp_sqrt_rn(dot(V, V), &root), V);   // u | td
+                        if (isdiff) {
+                            specular = false;
+                            thr = mul(thr, cc);
+                            diff = true;              // shadow rays: below, compacted over the wave
+                            rd = cosine_tail<true>(nl, U, q0, q1, s1, SCT);
+                        } else {
+                            const float aa = nt - nc, bb = nt + nc;
+                            const float R0 = aa * aa / (bb * bb);
+                            const float c = 1 - (into ? -ddn : dot(U, normal));
+                            const float Re = R0 + (1 - R0) * c * c * c * c * c;
+                            const float Tr = 1.f - Re;
+                            const float Pp = .25f + .5f * Re;
+                            const bool reflect = q2 < Pp;
+                            const float k = (reflect ? Re : Tr) / (reflect ? Pp : 1.f - Pp);
+                            thr = mul(smul(k, thr), cc);
+                            rd = reflect ? refl : U;
+                        }
+                    }
+                    ro = hit;
+                }
+#else
                 } else if ((mat & 255) == BDPT_DEV_DIFF) {               // :663-703
                     specular = false;
                     thr = mul(thr, mk(cm.x, cm.y, cm.z));
@@ -699,6 +787,7 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                     }
                     ro = hit;
                 }
+#endif
             }
         }
 
