@@ -151,6 +151,23 @@ __device__ __forceinline__ float sphere_isect_inf(float4 g, f3 o, f3 d) {
     return r > kEps ? r : __builtin_inff();
 }
 
+// The two roots of the same test, t1 <= t2 (fl is monotone and the root is >= 0; both NaN for a
+// negative det).  With r = t1 > EPS ? t1 : t2, the reference's hit (t1 > EPS ? t1 : t2 > EPS ?
+// t2 : miss) is "r if t2 > EPS": when t1 > EPS, t2 >= t1 > EPS too.  So the closest-hit update is
+// `t2 > EPS && r < t` and the shadow test `t2 > EPS && r < maxt`: one select fewer than with the
+// +inf miss encoding (two compares and a select instead of two selects and a compare).
+struct troots { float t1, t2; };
+__device__ __forceinline__ troots sphere_roots(float4 g, f3 o, f3 d) {
+    f3 op = mk(g.x - o.x, g.y - o.y, g.z - o.z);
+    float b = dot(op, d);
+    float det = b * b - dot(op, op) + g.w;
+    const float s = bdpt_sqrt_rn_core(det);
+    return {b - s, b + s};
+}
+#ifndef BDPT_T2VALID
+#define BDPT_T2VALID 1
+#endif
+
 // UniformSampleSphereDevice device.cu:157-165
 template <bool TAB = false>
 __device__ __forceinline__ f3 uniform_sphere(float u1, float u2, const double* tab = nullptr) {
@@ -657,11 +674,20 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                     }
                 }
             } else {
+#if BDPT_T2VALID
+#pragma unroll kUnroll
+                for (int s = n - 1; s >= 0; --s) {
+                    const troots q = sphere_roots(geom(s), ro, rd);
+                    const float r = q.t1 > kEps ? q.t1 : q.t2;
+                    if (q.t2 > kEps && r < t) { t = r; id = s; }
+                }
+#else
 #pragma unroll kUnroll
                 for (int s = n - 1; s >= 0; --s) {
                     const float d = sphere_isect_inf(geom(s), ro, rd);
                     if (d < t) { t = d; id = s; }
                 }
+#endif
             }
             done = id < 0;
             if (!done) {
@@ -901,8 +927,14 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                                 const f3 o = mk(r0.x, r0.y, r0.z), d = mk(r1.x, r1.y, r1.z);
                                 const bool vac = r1.w != 0.f;
                                 for (int s = n - 1 - g; s >= 0; s -= 1 << lg) {
+#if BDPT_T2VALID
+                                    const troots q = sphere_roots(G[s], o, d);
+                                    const float rr = q.t1 > kEps ? q.t1 : q.t2;
+                                    if (q.t2 > kEps && rr < r0.w && !(vac && emissive(s))) { occ = 1; break; }
+#else
                                     const float dd = sphere_isect_inf(G[s], o, d);
                                     if (dd < r0.w && !(vac && emissive(s))) { occ = 1; break; }
+#endif
                                 }
                             }
                             unsigned long long m = __builtin_amdgcn_ballot_w64(occ != 0);
@@ -952,8 +984,16 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                         const unsigned long long vacm = __builtin_amdgcn_ballot_w64(vac);
                         unsigned long long occm = 0;
                         auto step = [&](int s) -> bool {                  // IntersectP(Vacuum)Device
+#if BDPT_T2VALID
+                            const troots q = sphere_roots(geom(s), o, d);
+                            const float rr = q.t1 > kEps ? q.t1 : q.t2;
+                            // two ballots: a ballot of `a && b` is materialised through a VGPR
+                            unsigned long long h = __builtin_amdgcn_ballot_w64(q.t2 > kEps) &
+                                                   __builtin_amdgcn_ballot_w64(rr < r0.w);
+#else
                             const float dd = sphere_isect_inf(geom(s), o, d);
                             unsigned long long h = __builtin_amdgcn_ballot_w64(dd < r0.w);
+#endif
                             if (emissive(s)) h &= ~vacm;
                             occm |= h;
                             return occm != live;
