@@ -83,6 +83,7 @@ struct bdpt_path_args {
     int bvh_nn, bvh_ns, big_n;
     float bvh_c[3], bvh_r;          // ball around every BVH sphere (per-ray margin)
     float bvh_q;                    // 64u / smallest BVH radius (per-ray margin)
+    unsigned long long* prof;       // BDPT_PROF builds: per-section shader cycles (8 counters)
 };
 
 // Tile row of a workgroup row: identity, or the sub-th tile row of this shard's k-th band.

@@ -56,6 +56,7 @@ struct bdpt_ctx {
     // has read it.  Everything else that touches colors/counter/pixels runs on `stream` after
     // join_fold() has made it wait for the last fold.
     hipStream_t fstream = nullptr;
+    unsigned long long* d_prof = nullptr;   // BDPT_PROF=1 (with a -DBDPT_PROF kernel): section cycles
     hipEvent_t rb_path_ev[2] = {nullptr, nullptr};   // path kernel of the half done (stream)
     hipEvent_t rb_fold_ev[2] = {nullptr, nullptr};   // fold of the half done (fstream)
     bool rb_used[2] = {false, false};
@@ -692,6 +693,17 @@ void bdpt_destroy(bdpt_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->fstream) (void)hipStreamSynchronize(c->fstream);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->d_prof) {                 // section profile of a -DBDPT_PROF kernel (experiments)
+        unsigned long long p[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (hipMemcpy(p, c->d_prof, sizeof p, hipMemcpyDeviceToHost) == hipSuccess) {
+            double tot = 0;
+            for (int q = 0; q < 6; q++) tot += (double)p[q];
+            fprintf(stderr, "bdpt_prof waves=%llu cycles/wave=%.0f", p[7], p[7] ? tot / p[7] : 0.0);
+            for (int q = 0; q < 6; q++) fprintf(stderr, " s%d=%.4f", q, tot > 0 ? p[q] / tot : 0.0);
+            fprintf(stderr, "\n");
+        }
+        (void)hipFree(c->d_prof);
+    }
     release(c);
     delete c;
 }
@@ -901,6 +913,11 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
     memcpy(a.ux, ux, sizeof(ux)); memcpy(a.uy, uy, sizeof(uy)); memcpy(a.ud, ud, sizeof(ud));
     a.orig[0] = cam.orig.x; a.orig[1] = cam.orig.y; a.orig[2] = cam.orig.z;
     a.shard = c->shard; a.nshards = c->nshards; a.band_rows = c->band_rows;
+    if (!c->d_prof && getenv("BDPT_PROF")) {
+        HIPCHK(c, hipMalloc(&c->d_prof, 8 * sizeof(unsigned long long)));
+        HIPCHK(c, hipMemset(c->d_prof, 0, 8 * sizeof(unsigned long long)));
+    }
+    a.prof = c->d_prof;
 
     // Grid rows: every tile row, or (bands a whole number of tile rows) only this shard's bands.
     const int tile_rows = (c->H + BDPT_BTH - 1) / BDPT_BTH;

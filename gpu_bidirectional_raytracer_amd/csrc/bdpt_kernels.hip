@@ -368,6 +368,23 @@ __device__ __forceinline__ float4 ld_const(const float4* p, int i) {
 #endif
 }
 
+// d_Rand[j .. j+4] (device.cu:619): five dword loads, or (BDPT_RAND_X4) one dwordx4 + one dword
+// through a 4-byte-aligned vector type.  BDPT_ABL_RNG (ablation, changes results): no loads,
+// a hash of j instead -- the cost of the table reads.
+__device__ __forceinline__ void load_rand5(const float* __restrict__ rnd, unsigned j, float& q0,
+                                           float& q1, float& q2, float& q3, float& q4) {
+#if defined(BDPT_ABL_RNG)
+    auto h = [](unsigned v) { v *= 2654435761u; v ^= v >> 15; return ((v >> 8) | 1u) * 0x1p-24f; };
+    q0 = h(j); q1 = h(j + 1); q2 = h(j + 2); q3 = h(j + 3); q4 = h(j + 4);
+#elif defined(BDPT_RAND_X4)
+    typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
+    const f4u v = *(const f4u*)(rnd + j);
+    q0 = v.x; q1 = v.y; q2 = v.z; q3 = v.w; q4 = rnd[j + 4];
+#else
+    q0 = rnd[j]; q1 = rnd[j + 1]; q2 = rnd[j + 2]; q3 = rnd[j + 3]; q4 = rnd[j + 4];
+#endif
+}
+
 // f(S), f(S-1), ..., f(0) with compile-time indices while f returns true
 template <int S, typename F>
 __device__ __forceinline__ void unroll_down(F& f) {
@@ -569,6 +586,15 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
     auto tabP = [&](int s) -> float4 { if constexpr (kBVH) return a.mat[3 * s + 2]; else return P[s]; };
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#ifdef BDPT_PROF
+    // section profile (experiments): shader cycles per wave between wave-uniform points, summed
+    // per section and added to a.prof by lane 0 at the end (s_memtime waits on lgkmcnt, so the
+    // profile perturbs LDS overlap a little)
+    unsigned long long pacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pt = __builtin_amdgcn_s_memtime();
+#define BDPT_TICK(k) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); pacc[k] += t_ - pt; pt = t_; } while (0)
+#else
+#define BDPT_TICK(k) do { } while (0)
+#endif
     const int x = blockIdx.x * BDPT_BTW + (wave % BDPT_BLOCK_WX) * BDPT_WTW + (lane % BDPT_WTW);
     const int ly = blockIdx.y * BDPT_BTH + (wave / BDPT_BLOCK_WX) * BDPT_WTH + (lane / BDPT_WTW);
     const int yoff = (bdpt_dev_tile_row(a, blockIdx.y) - (int)blockIdx.y) * BDPT_BTH;   // uniform
@@ -601,7 +627,8 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
     int k = 0;                        // slot: this lane renders pass s0 + k*S next
     unsigned depth = 0;
     unsigned j = (ibase + SID[0]) % M5;
-    float q0 = rnd[j], q1 = rnd[j + 1], q2 = rnd[j + 2], q3 = rnd[j + 3], q4 = rnd[j + 4];
+    float q0, q1, q2, q3, q4;
+    load_rand5(rnd, j, q0, q1, q2, q3, q4);
     f3 ro = mk(0.f, 0.f, 0.f), rd = ro, thr = ro, rad = ro, nl = ro;
     bool specular = true, fresh = true;
     bool alive = active && nslot > 0 && cnt0 + (unsigned)s0 < BDPT_DEV_COUNTER_CAP;
@@ -617,6 +644,8 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
         }
 #endif
         bool done = false, diff = false;
+        float t = 1e20f;
+        int id = -1;
         if (alive) {
             if (fresh) {                  // camera ray (:562-600); d_Rand[kk] == q0 (kk == j)
                 unsigned xyv = xy;
@@ -643,8 +672,6 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                 fresh = false;
             }
             // closest hit, scanning from the last sphere down (device.cu:106-124)
-            float t = 1e20f;
-            int id = -1;
             if constexpr (kBVH) {
                 // walls by brute force, then the BVH; equal distances go to the higher index,
                 // which is what the reference's downward scan with `d < t` yields
@@ -690,6 +717,9 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
 #endif
             }
             done = id < 0;
+        }
+        BDPT_TICK(0);                 // camera ray + closest hit
+        if (alive) {
             if (!done) {
                 const float4 cm = tabC(id);
                 const int mat = __float_as_int(cm.w);
@@ -817,6 +847,7 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
             }
         }
 
+        BDPT_TICK(1);                 // hit shading
         // ---- SampleLightsDevice (device.cu:457-542) for the diffuse vertices of this segment:
         // NEE towards every emitter (same d_Rand[j+3], d_Rand[j+4] for all) + 1 VLP, blended 1/2.
         if (__builtin_amdgcn_ballot_w64(diff) != 0) {
@@ -895,6 +926,7 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                     SQ[kQueue + pv] = make_float4(vsd.x, vsd.y, vsd.z, 1.f);
                 }
                 wave_lds_fence();
+                BDPT_TICK(2);         // NEE / VLP set-up and queue writes
 #ifdef BDPT_STATS
                 {
                     const unsigned long long md = __builtin_amdgcn_ballot_w64(diff);
@@ -1017,6 +1049,7 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                     }
                 }
                 wave_lds_fence();
+                BDPT_TICK(3);         // shadow rounds
                 if (has_nee && __float_as_uint(SQ[pn].w) == 0) res = add(res, con);
                 if (has_vlp && __float_as_uint(SQ[pv].w) != 0) vcon = mk(0.f, 0.f, 0.f);
                 if (li == 0 && !has_vlp) vcon = mk(0.f, 0.f, 0.f);
@@ -1032,6 +1065,7 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
             }
         }
 
+        BDPT_TICK(4);                 // shadow results + contribution
         if (alive) {
             if (!done && ++depth > 6) done = true;                       // :621 7-segment cap
             if (done) {                                                  // :774-787
@@ -1067,10 +1101,17 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                 asm volatile("" : "+v"(xyv));
                 const unsigned li = (xyv >> 16) * (unsigned)a.W + (xyv & 0xffffu);
                 j = (26u + li * 25u + depth * 5u + SID[k]) % M5;
-                q0 = rnd[j]; q1 = rnd[j + 1]; q2 = rnd[j + 2]; q3 = rnd[j + 3]; q4 = rnd[j + 4];
+                load_rand5(rnd, j, q0, q1, q2, q3, q4);
             }
         }
+        BDPT_TICK(5);                 // path end / accumulation / RNG prefetch
     }
+#ifdef BDPT_PROF
+    if (lane == 0 && a.prof) {
+        for (int q = 0; q < 6; q++) atomicAdd(&a.prof[q], pacc[q]);
+        atomicAdd(&a.prof[7], 1ull);
+    }
+#endif
     if (STREAMS || !active || k == 0) return;                            // nothing rendered
     const unsigned cnt = cnt0 + (unsigned)k;
     bdpt_dev_vec out;
@@ -1096,6 +1137,15 @@ extern "C" const void* bdpt_path_kernel_table[36] = {BDPT_ROW(false), BDPT_ROW(t
 // rows (and shard remap) as the path launch; one thread per pixel.
 extern "C" __global__ __launch_bounds__(256) void bdpt_accum_kernel(bdpt_path_args a) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#ifdef BDPT_PROF
+    // section profile (experiments): shader cycles per wave between wave-uniform points, summed
+    // per section and added to a.prof by lane 0 at the end (s_memtime waits on lgkmcnt, so the
+    // profile perturbs LDS overlap a little)
+    unsigned long long pacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pt = __builtin_amdgcn_s_memtime();
+#define BDPT_TICK(k) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); pacc[k] += t_ - pt; pt = t_; } while (0)
+#else
+#define BDPT_TICK(k) do { } while (0)
+#endif
     const int x = blockIdx.x * BDPT_BTW + (wave % BDPT_BLOCK_WX) * BDPT_WTW + (lane % BDPT_WTW);
     const int ly = blockIdx.y * BDPT_BTH + (wave / BDPT_BLOCK_WX) * BDPT_WTH + (lane / BDPT_WTW);
     const int y = bdpt_dev_tile_row(a, blockIdx.y) * BDPT_BTH + (ly - blockIdx.y * BDPT_BTH);

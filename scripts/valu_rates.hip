@@ -123,6 +123,32 @@ __global__ __launch_bounds__(256) void t_fma_f64(float* out, int iters, unsigned
     out[blockIdx.x * 256 + threadIdx.x] = (float)(d0 + d1 + d2 + d3);
 }
 
+// f32 -> f64 -> op -> f32 chains (register pairs)
+#define F64KERNEL(NAME, BODY)                                                                       \
+    __global__ __launch_bounds__(256) void NAME(float* out, int iters, unsigned long long* clk) {   \
+        float a0 = threadIdx.x + 1, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3;                          \
+        double d0 = a0, d1 = a1, d2 = a2, d3 = a3;                                                  \
+        const unsigned long long t0 = __builtin_amdgcn_s_memtime();                                 \
+        for (int it = 0; it < iters; it++) {                                                        \
+            _Pragma("unroll") for (int k = 0; k < kInner * 2; k++)                                  \
+                asm volatile(BODY : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(d0), "+v"(d1),      \
+                             "+v"(d2), "+v"(d3));                                                   \
+        }                                                                                           \
+        const unsigned long long t1 = __builtin_amdgcn_s_memtime();                                 \
+        if (threadIdx.x == 0 && blockIdx.x == 0) clk[0] = t1 - t0;                                  \
+        out[blockIdx.x * 256 + threadIdx.x] = a0 + a1 + a2 + a3 + (float)(d0 + d1 + d2 + d3);      \
+    }
+F64KERNEL(t_cvt_f64_f32, "v_cvt_f64_f32 %4, %0\n v_cvt_f64_f32 %5, %1\n v_cvt_f64_f32 %6, %2\n v_cvt_f64_f32 %7, %3\n")
+F64KERNEL(t_cvt_f32_f64, "v_cvt_f32_f64 %0, %4\n v_cvt_f32_f64 %1, %5\n v_cvt_f32_f64 %2, %6\n v_cvt_f32_f64 %3, %7\n")
+F64KERNEL(t_sqrt_f64, "v_sqrt_f64 %4, %4\n v_sqrt_f64 %5, %5\n v_sqrt_f64 %6, %6\n v_sqrt_f64 %7, %7\n")
+F64KERNEL(t_rsq_f64, "v_rsq_f64 %4, %4\n v_rsq_f64 %5, %5\n v_rsq_f64 %6, %6\n v_rsq_f64 %7, %7\n")
+F64KERNEL(t_rcp_f64, "v_rcp_f64 %4, %4\n v_rcp_f64 %5, %5\n v_rcp_f64 %6, %6\n v_rcp_f64 %7, %7\n")
+F64KERNEL(t_mul_f64, "v_mul_f64 %4, %4, %5\n v_mul_f64 %5, %5, %6\n v_mul_f64 %6, %6, %7\n v_mul_f64 %7, %7, %4\n")
+F64KERNEL(t_add_f64, "v_add_f64 %4, %4, %5\n v_add_f64 %5, %5, %6\n v_add_f64 %6, %6, %7\n v_add_f64 %7, %7, %4\n")
+F64KERNEL(t_rsq_f32, "v_rsq_f32 %0, %0\n v_rsq_f32 %1, %1\n v_rsq_f32 %2, %2\n v_rsq_f32 %3, %3\n")
+F64KERNEL(t_rndne_f64, "v_rndne_f64 %4, %4\n v_rndne_f64 %5, %5\n v_rndne_f64 %6, %6\n v_rndne_f64 %7, %7\n")
+F64KERNEL(t_cvt_i32_f64, "v_cvt_i32_f64 %0, %4\n v_cvt_i32_f64 %1, %5\n v_cvt_i32_f64 %2, %6\n v_cvt_i32_f64 %3, %7\n")
+
 typedef void (*kfn)(float*, int, unsigned long long*);
 struct T { const char* name; kfn f; int instr_per_inner; };
 
@@ -143,7 +169,11 @@ int main(int argc, char** argv) {
         {"v_cmp_gt_f32 e64 s[0:1]", t_cmp_e64f, 8}, {"v_cvt_f32_u32", t_cvt_f32_u32, 8},
         {"v_mul_hi_u32", t_mul_hi, 8}, {"v_mul_lo_u32", t_mul_lo, 8}, {"v_add_f32 sgpr", t_add_f32_s, 8},
         {"v_max_i32", t_max_i32, 8}, {"v_add_u32", t_add_u32, 8}, {"v_lshl_add_u32", t_lshl_add, 8},
-        {"v_cmp_lt_f32 vcc", t_cmp_vcc, 8}};
+        {"v_cmp_lt_f32 vcc", t_cmp_vcc, 8},
+        {"v_cvt_f64_f32", t_cvt_f64_f32, 8}, {"v_cvt_f32_f64", t_cvt_f32_f64, 8},
+        {"v_sqrt_f64", t_sqrt_f64, 8}, {"v_rsq_f64", t_rsq_f64, 8}, {"v_rcp_f64", t_rcp_f64, 8},
+        {"v_mul_f64", t_mul_f64, 8}, {"v_add_f64", t_add_f64, 8}, {"v_rsq_f32", t_rsq_f32, 8},
+        {"v_rndne_f64", t_rndne_f64, 8}, {"v_cvt_i32_f64", t_cvt_i32_f64, 8}};
     int dev = 0, cus = 0;
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     float* out;
