@@ -219,6 +219,9 @@ __device__ __forceinline__ f3 cosine_tail(f3 w, f3 u, float u_phi, float u_r2, f
 #ifndef BDPT_MERGE_REFR
 #define BDPT_MERGE_REFR 1
 #endif
+#ifndef BDPT_PACK_EDGES
+#define BDPT_PACK_EDGES 1
+#endif
 
 }  // namespace
 
@@ -595,8 +598,30 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
 #else
 #define BDPT_TICK(k) do { } while (0)
 #endif
-    const int x = blockIdx.x * BDPT_BTW + (wave % BDPT_BLOCK_WX) * BDPT_WTW + (lane % BDPT_WTW);
-    const int ly = blockIdx.y * BDPT_BTH + (wave / BDPT_BLOCK_WX) * BDPT_WTH + (lane / BDPT_WTW);
+    int x = blockIdx.x * BDPT_BTW + (wave % BDPT_BLOCK_WX) * BDPT_WTW + (lane % BDPT_WTW);
+    int ly = blockIdx.y * BDPT_BTH + (wave / BDPT_BLOCK_WX) * BDPT_WTH + (lane / BDPT_WTW);
+#if BDPT_PACK_EDGES
+    // Frame edges packed into full waves (rows not remapped to shard bands): a frame whose width
+    // leaves tw <= 8 columns in the last workgroup column (1921 = 60 x 32 + 1) would give every
+    // tile row one wave with tw x 8 live lanes that still runs whole paths; instead those tw x H
+    // pixels are dealt out y-major, 256 per workgroup of that column, and likewise the th < 8
+    // rows of the last workgroup row (x below the last column, row-major) to the workgroups of
+    // that row.  Every pixel is still rendered by exactly one lane.
+    if (a.tiles_per_band <= 0) {
+        const int gx = (int)gridDim.x, gy = (int)gridDim.y;
+        const int xt = (gx - 1) * BDPT_BTW, yt = (gy - 1) * BDPT_BTH;
+        const int tw = a.W - xt, th = a.H - yt, wl = (int)threadIdx.x;
+        if (tw <= BDPT_WTW && (int)blockIdx.x == gx - 1) {
+            const int q = (int)blockIdx.y * 256 + wl;
+            x = xt + q % tw;
+            ly = q / tw;
+        } else if (th < BDPT_BTH && (int)blockIdx.x < gx - 1 && (int)blockIdx.y == gy - 1) {
+            const int q = (int)blockIdx.x * 256 + wl;
+            x = q % xt;
+            ly = yt + q / xt;
+        }
+    }
+#endif
     const int yoff = (bdpt_dev_tile_row(a, blockIdx.y) - (int)blockIdx.y) * BDPT_BTH;   // uniform
     const int y = ly + yoff;
     bool active = x < a.W && y < a.H;
