@@ -463,6 +463,16 @@ def test_template_boundary_16_17_spheres(gpu, rnd0, n):
     _render_vs_oracle(gpu, rnd0, cam, np.ascontiguousarray(sp[-n:]), 31, 21, 4)
 
 
+# Frame shapes for the packed edges (bdpt_kernels.hip BDPT_PACK_EDGES, tests/test_pixel_mapping.py):
+# last workgroup column of <= 8 columns and/or last workgroup row of < 8 rows, both, neither, and
+# a wide last column beside a packed last row (the corner workgroup keeps its own tile).
+@pytest.mark.parametrize("W,H,streams", [(121, 89, 0), (121, 89, 1), (33, 17, 0), (40, 8, 0), (9, 3, 1),
+                                         (64, 24, 0), (65, 25, 1), (100, 33, 0)])
+def test_edge_packing_shapes(gpu, rnd0, W, H, streams):
+    cam, sp = scene("cornell_glass")
+    _render_vs_oracle(gpu, rnd0, cam, sp, W, H, 3, streams=streams)
+
+
 @pytest.mark.parametrize("W,H", [(1921, 1), (1, 301), (37, 9)])
 def test_thin_frames(gpu, rnd0, W, H):
     cam, sp = scene("cornell_glass")
