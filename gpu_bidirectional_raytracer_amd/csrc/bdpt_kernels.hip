@@ -222,6 +222,10 @@ __device__ __forceinline__ f3 cosine_tail(f3 w, f3 u, float u_phi, float u_r2, f
 #ifndef BDPT_PACK_EDGES
 #define BDPT_PACK_EDGES 1
 #endif
+// camera terms: per-lane fp64 base in LDS, kz products formed once per workgroup
+#ifndef BDPT_CAMB
+#define BDPT_CAMB 1
+#endif
 
 }  // namespace
 
@@ -556,7 +560,12 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
     if (threadIdx.x == 0) {
         K[0] = make_float4(a.ux[0], a.ux[1], a.ux[2], a.tx);
         K[1] = make_float4(a.uy[0], a.uy[1], a.uy[2], a.ty);
+#if BDPT_CAMB
+        // kz * ud and tz * kz (kz = 10, device.cu:583-590): the same products, formed once
+        K[2] = make_float4(10.0f * a.ud[0], 10.0f * a.ud[1], 10.0f * a.ud[2], a.tz * 10.0f);
+#else
         K[2] = make_float4(a.ud[0], a.ud[1], a.ud[2], a.tz);
+#endif
         K[3] = make_float4(a.orig[0], a.orig[1], a.orig[2], 0.f);
         K[4] = make_float4(a.inv_w, a.inv_h, 0.f, 0.f);
     }
@@ -629,6 +638,13 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
     // Pass p = s0 + k*S (slot k) is rendered iff counter0 + p < 30000 (one increment per pass).
     float4* SQ = Q + wave * kQueue * 2;
 
+#if BDPT_CAMB
+    // this lane's camera terms ((double)((float)x * iw) - iw*W/2., same for y) of device.cu:565-566,
+    // formed once per launch instead of once per pass
+    __shared__ double2 camb[256];
+    camb[threadIdx.x] = make_double2((double)((float)x * a.inv_w) - a.half_w,
+                                     (double)((float)y * a.inv_h) - a.half_h);
+#endif
     const int i = active ? y * a.W + x : 0;
     const unsigned ibase = 26u + (unsigned)(i * 25);
     // The pixel coordinates live in one packed register (W, H < 2^16, bdpt_create) and are
@@ -673,10 +689,21 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
         int id = -1;
         if (alive) {
             if (fresh) {                  // camera ray (:562-600); d_Rand[kk] == q0 (kk == j)
+                const float4 c0 = K[0], c1 = K[1], c2 = K[2], c3 = K[3], k4 = K[4];
+#if BDPT_CAMB
+                // device.cu:565-566: ((float)x*iw - iw*W/2.) + d_Rand[kk]*iw in fp64, then fp32
+                const double2 cb = camb[threadIdx.x];
+                const float kx = (float)(cb.x + (double)(q0 * k4.x));
+                const float ky = (float)(cb.y + (double)(q1 * k4.y));
+                f3 rdir = mk(0.f, 0.f, 0.f);
+                rdir = add(rdir, smul(kx, mk(c0.x, c0.y, c0.z)));
+                rdir = add(rdir, smul(ky, mk(c1.x, c1.y, c1.z)));
+                rdir = add(rdir, mk(c2.x, c2.y, c2.z));                       // kz * ud
+                const float w = (c0.w * kx + c1.w * ky + c2.w) + 1;           // c2.w = tz * kz
+#else
                 unsigned xyv = xy;
                 asm volatile("" : "+v"(xyv));
                 const int x = (int)(xyv & 0xffffu), y = (int)(xyv >> 16);
-                const float4 c0 = K[0], c1 = K[1], c2 = K[2], c3 = K[3], k4 = K[4];
                 // device.cu:565-566: ((float)x*iw - iw*W/2.) + d_Rand[kk]*iw in fp64, then fp32
                 const float kx = (float)(((double)((float)x * k4.x) - a.half_w) + (double)(q0 * k4.x));
                 const float ky = (float)(((double)((float)y * k4.y) - a.half_h) + (double)(q1 * k4.y));
@@ -686,6 +713,7 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                 rdir = add(rdir, smul(ky, mk(c1.x, c1.y, c1.z)));
                 rdir = add(rdir, smul(kz, mk(c2.x, c2.y, c2.z)));
                 const float w = (c0.w * kx + c1.w * ky + c2.w * kz) + 1;
+#endif
                 // (float)(1./(double)w) == 1.f/w: double rounding of a quotient is innocuous
                 // when 53 >= 2*24 + 2 (device.cu:594)
                 rdir = smul(rcp_rn(w), rdir);
