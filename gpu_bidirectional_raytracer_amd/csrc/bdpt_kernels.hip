@@ -729,9 +729,10 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                 // walls by brute force, then the BVH; equal distances go to the higher index,
                 // which is what the reference's downward scan with `d < t` yields
                 for (int q = a.big_n - 1; q >= 0; --q) {
-                    const float d = sphere_isect_inf(BG[q], ro, rd);
+                    const troots h = sphere_roots(BG[q], ro, rd);
+                    const float d = h.t1 > kEps ? h.t1 : h.t2;
                     const int s = BI[q] & kBvhIdMask;
-                    if (d < t || (d == t && s > id)) { t = d; id = s; }
+                    if (h.t2 > kEps && (d < t || (d == t && s > id))) { t = d; id = s; }
                 }
                 const bvh_ray br = bvh_setup(a, ro, rd);
                 int node = 0;
@@ -748,9 +749,10 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                     if (info < 0) break;
                     const int first = info & 0xffffff, end = first + (info >> 24);
                     for (int k = first; k < end; k++) {
-                        const float d = sphere_isect_inf(SGt[k], ro, rd);
+                        const troots h = sphere_roots(SGt[k], ro, rd);
+                        const float d = h.t1 > kEps ? h.t1 : h.t2;
                         const int s = SIt[k] & kBvhIdMask;
-                        if (d < t || (d == t && s > id)) { t = d; id = s; }
+                        if (h.t2 > kEps && (d < t || (d == t && s > id))) { t = d; id = s; }
                     }
                 }
             } else {
@@ -1041,8 +1043,9 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
 #endif
                         if constexpr (kBVH) {                             // IntersectP(Vacuum)Device
                             for (int q = 0; q < a.big_n && !occ; q++) {
-                                const float dd = sphere_isect_inf(BG[q], o, d);
-                                if (dd < r0.w && !(vac && (BI[q] & kBvhEmissive))) occ = 1;
+                                const troots h = sphere_roots(BG[q], o, d);
+                                const float dd = h.t1 > kEps ? h.t1 : h.t2;
+                                if (h.t2 > kEps && dd < r0.w && !(vac && (BI[q] & kBvhEmissive))) occ = 1;
                             }
                             const bvh_ray br = bvh_setup(a, o, d);
                             int node = occ ? a.bvh_nn : 0;
@@ -1053,8 +1056,9 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                                 if (info < 0) { node++; continue; }
                                 const int first = info & 0xffffff, end = first + (info >> 24);
                                 for (int k = first; k < end; k++) {
-                                    const float dd = sphere_isect_inf(SGt[k], o, d);
-                                    if (dd < r0.w && !(vac && (SIt[k] & kBvhEmissive))) { occ = 1; break; }
+                                    const troots h = sphere_roots(SGt[k], o, d);
+                                    const float dd = h.t1 > kEps ? h.t1 : h.t2;
+                                    if (h.t2 > kEps && dd < r0.w && !(vac && (SIt[k] & kBvhEmissive))) { occ = 1; break; }
                                 }
                                 node = occ ? a.bvh_nn : __float_as_int(lo.w);
                             }
