@@ -183,6 +183,24 @@ __device__ __forceinline__ troots sphere_roots(float4 g, f3 o, f3 d) {
 #ifndef BDPT_T2VALID
 #define BDPT_T2VALID 1
 #endif
+// The same test in two steps, so that a wave can stop after `det` when no lane's det is >= 0 (or
+// NaN): every such lane misses (the reference returns 0 for det < 0, device.cu:95), so the root,
+// its correction, the two roots and the selects of that sphere are skipped for the whole wave.
+// Specialised kernels use it for the non-wall spheres (radius < 1000: for a wall every line hits),
+// where most waves' rays all miss the sphere's line.
+struct tdet { float b, det; };
+__device__ __forceinline__ tdet sphere_det(float4 g, f3 o, f3 d) {
+    f3 op = mk(g.x - o.x, g.y - o.y, g.z - o.z);
+    float b = dot(op, d);
+    return {b, b * b - dot(op, op) + g.w};
+}
+__device__ __forceinline__ troots roots_of(tdet q) {
+    const float s = bdpt_sqrt_rn_core(q.det);
+    return {q.b - s, q.b + s};
+}
+#ifndef BDPT_DET_SKIP
+#define BDPT_DET_SKIP 1
+#endif
 
 // UniformSampleSphereDevice device.cu:157-165
 template <bool TAB = false>
@@ -608,6 +626,14 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
         if constexpr (N > 0) return (a.emis_mask >> s) & 1u;
         else return (__float_as_int(C[s].w) & 256) != 0;
     };
+    // spheres worth a wave-uniform det test (BDPT_DET_SKIP): non-walls of a specialised kernel
+    auto small_sphere = [&](int s) -> bool {
+#ifdef BDPT_JIT
+        if constexpr (N == BDPT_JIT_N) return kJitGeom[s].w < 1e6f;
+#endif
+        (void)s;
+        return false;
+    };
     // per-lane hit data: LDS tables, or (BVH scenes, too large for LDS) the global copy
     auto tabC = [&](int s) -> float4 { if constexpr (kBVH) return a.mat[3 * s]; else return C[s]; };
     auto tabE = [&](int s) -> float4 { if constexpr (kBVH) return a.mat[3 * s + 1]; else return E[s]; };
@@ -772,7 +798,27 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                     }
                 }
             } else {
-#if BDPT_T2VALID
+#if BDPT_T2VALID && BDPT_DET_SKIP && defined(BDPT_JIT)
+                if constexpr (N == BDPT_JIT_N) {
+                    auto hit = [&](int s) -> bool {
+                        const tdet qd = sphere_det(geom(s), ro, rd);
+                        if (small_sphere(s) && __builtin_amdgcn_ballot_w64(!(qd.det < 0.f)) == 0)
+                            return true;                          // every lane misses sphere s
+                        const troots q = roots_of(qd);
+                        const float r = q.t1 > kEps ? q.t1 : q.t2;
+                        if (q.t2 > kEps && r < t) { t = r; id = s; }
+                        return true;
+                    };
+                    unroll_down<N - 1>(hit);
+                } else {
+#pragma unroll kUnroll
+                    for (int s = n - 1; s >= 0; --s) {
+                        const troots q = sphere_roots(geom(s), ro, rd);
+                        const float r = q.t1 > kEps ? q.t1 : q.t2;
+                        if (q.t2 > kEps && r < t) { t = r; id = s; }
+                    }
+                }
+#elif BDPT_T2VALID
 #pragma unroll kUnroll
                 for (int s = n - 1; s >= 0; --s) {
                     const troots q = sphere_roots(geom(s), ro, rd);
@@ -1098,7 +1144,11 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                         unsigned long long occm = 0;
                         auto step = [&](int s) -> bool {                  // IntersectP(Vacuum)Device
 #if BDPT_T2VALID
-                            const troots q = sphere_roots(geom(s), o, d);
+                            const tdet qd = sphere_det(geom(s), o, d);
+                            if (BDPT_DET_SKIP && small_sphere(s) &&
+                                __builtin_amdgcn_ballot_w64(!(qd.det < 0.f)) == 0)
+                                return true;                          // every ray misses sphere s
+                            const troots q = roots_of(qd);
                             const float rr = q.t1 > kEps ? q.t1 : q.t2;
                             // two ballots: a ballot of `a && b` is materialised through a VGPR
                             unsigned long long h = __builtin_amdgcn_ballot_w64(q.t2 > kEps) &
