@@ -516,6 +516,9 @@ static hipFunction_t jit_path_kernel(bdpt_ctx* c, bool streams) {
     const char* wenv = getenv("BDPT_JIT_WAVES");
     int waves = wenv ? atoi(wenv) : 6;
     const std::string name = "&bdpt_path_kernel_t<" + std::to_string(n) + (streams ? ", true>" : ", false>");
+    const char* jflags = getenv("BDPT_JIT_FLAGS");
+    const bool user_coarse = jflags && strstr(jflags, "BDPT_SC_COARSE");   // experiments decide
+    bool coarse = false;
     for (;; waves--) {
         const std::vector<std::string> opts = {
             "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize",
@@ -536,8 +539,24 @@ static hipFunction_t jit_path_kernel(bdpt_ctx* c, bool streams) {
                 }
             }
         }
+        if (coarse) all.push_back("-DBDPT_SC_COARSE=1");
         hipFunction_t fn = jit_build(c, name, all);
         if (!fn) return nullptr;
+        // The 4-KB sincos table costs a workgroup per CU when LDS bounds the count (large
+        // scenes: 16 B per sphere); then take the 2-KB table of even entries (bdpt_math.h).
+        // Estimated with one pass slot (bdpt_path_passes' smem formula).
+        int stat = 0;
+        if (!coarse && !user_coarse &&
+            hipFuncGetAttribute(&stat, HIP_FUNC_ATTRIBUTE_SHARED_SIZE_BYTES, fn) == hipSuccess) {
+            const size_t dyn = sizeof(float4) * (4 * (size_t)n + 3 + 5 + 4 * 128 * 2) + sizeof(unsigned);
+            const size_t lds = 160 * 1024, fine = lds / (dyn + stat), half = lds / (dyn + stat - 2048);
+            if (fine < (size_t)waves && half > fine) {
+                coarse = true;
+                waves++;                                      // same wave count, coarse table
+                continue;
+            }
+        }
+        (void)hipGetLastError();
         int scratch = 0;
         if (hipFuncGetAttribute(&scratch, HIP_FUNC_ATTRIBUTE_LOCAL_SIZE_BYTES, fn) != hipSuccess) {
             (void)hipGetLastError();

@@ -111,10 +111,10 @@ constexpr float kPi = 3.14159265358979323846f;             // geom.h:7 FLOAT_PI
 constexpr unsigned kRandN = BDPT_DEV_RAND_N;
 
 // the table of bdpt_sincos_tab in device memory (copied to LDS by the path kernel)
-__device__ const double bdpt_sincos_table_dev[256][2] = BDPT_SINCOS_TABLE_INIT;
+__device__ const double bdpt_sincos_table_dev[BDPT_SC_N][2] = BDPT_SINCOS_TABLE_INIT;
 
 // sinf/cosf with correctly-rounded semantics: fp64 sincos rounded once to fp32 (bdpt_math.h),
-// table-driven when the caller has the {sin, cos}(k pi/128) table in LDS.
+// table-driven when the caller has the sin(2pi k/N) table in LDS.
 #ifndef BDPT_SINCOS_TABLE
 #define BDPT_SINCOS_TABLE 1
 #endif
@@ -603,10 +603,14 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
         K[3] = make_float4(a.orig[0], a.orig[1], a.orig[2], 0.f);
         K[4] = make_float4(a.inv_w, a.inv_h, 0.f, 0.f);
     }
-    // sin(k pi/128) for the table-driven sincos (bdpt_math.h; cos(k pi/128) is entry k + 64),
-    // 2 KB, one entry per thread
-    __shared__ double sct[256];
-    sct[threadIdx.x] = bdpt_sincos_table_dev[threadIdx.x][0];
+    // sin(2pi k/N) for the table-driven sincos (bdpt_math.h; cos is entry k + N/4), 4 KB (2 KB
+    // with BDPT_SC_COARSE: every other entry)
+    constexpr int kSct = BDPT_SC_N >> BDPT_SC_COARSE;
+    __shared__ double sct[kSct];
+    static_assert(kSct % 256 == 0, "table fill");
+#pragma unroll
+    for (int q = 0; q < kSct; q += 256)
+        sct[q + threadIdx.x] = bdpt_sincos_table_dev[(q + threadIdx.x) << BDPT_SC_COARSE][0];
     const double* SCT = sct;
     __syncthreads();
 

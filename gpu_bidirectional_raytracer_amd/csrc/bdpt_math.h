@@ -47,21 +47,39 @@ BDPT_HD void bdpt_sincos_dp(double x, double* so, double* co) {
     *co = ((q + 1) & 2) ? -cs : cs;
 }
 
-// Table-driven fp64 sin & cos, cheaper than bdpt_sincos_dp (no quadrant logic, shorter
-// polynomials): k = rint(x * 128/pi), r = x - k*pi/128 (two-part constant, |r| <= pi/256),
+// Table-driven fp64 sin & cos, cheaper than bdpt_sincos_dp (no quadrant logic, short
+// polynomials): k = rint(x * N/2pi), r = x - k*2pi/N (two-part constant, |r| <= pi/N),
 // sin x = S_k cos r + C_k sin r, cos x = C_k cos r - S_k sin r with S_k = sintab[k] =
-// sin(k pi/128) and C_k = cos(k pi/128) = sintab[(k + 64) mod 256] (bdpt_sincos_table.h,
-// correctly rounded, so the two are the same double; the four axis entries exact).  For
-// 0 <= x <= 2pi (the render path's x = 2pi u).  Same exhaustive check as bdpt_sincos_dp
-// (tests/test_math.py).
+// sin(2pi k/N) and C_k = cos(2pi k/N) = sintab[(k + N/4) mod N] (bdpt_sincos_table.h, N = 512,
+// correctly rounded, so the two are the same double; the four axis entries exact).  With
+// |r| <= pi/512 the Taylor terms r^7/7! and r^6/6! are below 2^-56 relative and are dropped
+// (sin r = r - r^3/6 + r^5/120, cos r = 1 - r^2/2 + r^4/24).  For 0 <= x <= 2pi (the render
+// path's x = 2pi u).  BDPT_SC_COARSE = 1: the even entries only (N = 256, 2 KB of LDS instead of
+// 4 KB, for kernels whose LDS bounds the workgroups per CU); then r^6/6! is kept in cos r.  Same
+// exhaustive check as bdpt_sincos_dp for both (tests/test_math.py).
+#ifndef BDPT_SC_COARSE
+#define BDPT_SC_COARSE 0
+#endif
 BDPT_HD void bdpt_sincos_tab(double x, const double* sintab, double* so, double* co) {
+#if BDPT_SC_COARSE
+    // every other entry (N/2 = 256, 2 KB: LDS-bound kernels), |r| <= pi/256: cos r keeps r^6/6!
+    const int NT = BDPT_SC_N / 2;
+    const double kd = rint(x * (0.5 * BDPT_SC_INV));
+    const int k = ((int)kd) & (NT - 1);
+    const double r = fma(-kd, 2.0 * BDPT_SC_C2, fma(-kd, 2.0 * BDPT_SC_C1, x));
+    const double z = r * r;
+    const double sr = fma(r * z, fma(z, 1.0 / 120.0, -1.0 / 6.0), r);
+    const double cr = fma(z, fma(z, fma(z, -1.0 / 720.0, 1.0 / 24.0), -0.5), 1.0);
+#else
+    const int NT = BDPT_SC_N;
     const double kd = rint(x * BDPT_SC_INV);
-    const int k = ((int)kd) & 255;                    // k = 256 is x = 2pi: entry 0
+    const int k = ((int)kd) & (NT - 1);               // k = N is x = 2pi: entry 0
     const double r = fma(-kd, BDPT_SC_C2, fma(-kd, BDPT_SC_C1, x));
     const double z = r * r;
-    const double sr = fma(r * z, fma(z, fma(z, -1.0 / 5040.0, 1.0 / 120.0), -1.0 / 6.0), r);
-    const double cr = fma(z, fma(z, fma(z, -1.0 / 720.0, 1.0 / 24.0), -0.5), 1.0);
-    const double S = sintab[k], C = sintab[(k + 64) & 255];
+    const double sr = fma(r * z, fma(z, 1.0 / 120.0, -1.0 / 6.0), r);
+    const double cr = fma(z, fma(z, 1.0 / 24.0, -0.5), 1.0);
+#endif
+    const double S = sintab[k], C = sintab[(k + NT / 4) & (NT - 1)];
     *so = fma(S, cr, C * sr);
     *co = fma(C, cr, -(S * sr));
 }

@@ -9,6 +9,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include "../../gpu_bidirectional_raytracer_amd/csrc/bdpt_math.h"
+/* built twice by tests/test_math.py: -DBDPT_SC_COARSE=0 (512-entry table) and =1 (256) */
 
 int main(int argc, char **argv)
 {
@@ -17,9 +18,9 @@ int main(int argc, char **argv)
     uint32_t b0, b1;
     memcpy(&b0, &lo, 4);
     memcpy(&b1, &hi, 4);
-    static const double tab[256][2] = BDPT_SINCOS_TABLE_INIT;
-    double sintab[256];                     /* the device's LDS copy: sin(k pi/128) only */
-    for (int k = 0; k < 256; k++) sintab[k] = tab[k][0];
+    static const double tab[BDPT_SC_N][2] = BDPT_SINCOS_TABLE_INIT;
+    double sintab[BDPT_SC_N];               /* the device's LDS copy: sin(2pi k/N) only */
+    for (int k = 0; k < (BDPT_SC_N >> BDPT_SC_COARSE); k++) sintab[k] = tab[k << BDPT_SC_COARSE][0];
     long n = 0, bad = 0, bad_tab = 0;
     for (uint64_t b = b0; b <= b1; b += stride) {
         uint32_t bb = (uint32_t)b;
