@@ -201,6 +201,9 @@ __device__ __forceinline__ troots roots_of(tdet q) {
 #ifndef BDPT_DET_SKIP
 #define BDPT_DET_SKIP 1
 #endif
+#ifndef BDPT_NEE_MARKSTEIN
+#define BDPT_NEE_MARKSTEIN 1
+#endif
 
 // UniformSampleSphereDevice device.cu:157-165
 template <bool TAB = false>
@@ -1015,7 +1018,21 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                         if (wi > 0.f) {
                             has_nee = true;
                             maxt = len - kEps;
-                            con = smul(le.w * wi * wo / (len * len), mk(le.x, le.y, le.z));
+                            const float na = le.w * wi * wo, nb = len * len;
+#if BDPT_NEE_MARKSTEIN
+                            // one Markstein step (div_rn_normal) when a, b lie in [2^-60, 2^60]:
+                            // then 1/b, a/b and the residual stay normal; otherwise (grazing
+                            // wi * wo) the library division on an exec-masked branch
+                            float kq;
+                            if (__builtin_expect(na >= 0x1p-60f && na <= 0x1p60f &&
+                                                 nb >= 0x1p-60f && nb <= 0x1p60f, 1))
+                                kq = div_rn_normal(na, nb);
+                            else
+                                kq = na / nb;
+#else
+                            const float kq = na / nb;
+#endif
+                            con = smul(kq, mk(le.x, le.y, le.z));
                         }
                     }
                 }
