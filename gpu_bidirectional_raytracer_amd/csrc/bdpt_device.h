@@ -15,6 +15,10 @@
 #endif
 
 #define BDPT_DEV_RAND_N (4096u * 1876u)
+// d_Rand in 25 + 4 planes (bdpt_rand_planar_kernel): plane p < 25 holds d_Rand[25 q + p] at q,
+// plane 25 + t holds d_Rand[25 (q + 1) + t]; PL = ceil(RAND_N / 25) entries per plane
+#define BDPT_DEV_RANDP_PL 307364u
+#define BDPT_DEV_RANDP_PLANES 29u
 #define BDPT_DEV_N_PER_RNG 1876
 #define BDPT_DEV_LIGHT_POINTS 4096
 #define BDPT_DEV_COUNTER_CAP 30000u
@@ -55,6 +59,7 @@ struct bdpt_path_args {
     const float4* geom;             // per sphere {p, rad*rad} (SGPR-resident traversal)
     unsigned emis_mask;             // bit s = sphere s is emissive (sphere counts <= 32)
     const float* rnd;
+    const float* rndp;              // the planar copy (BDPT_DEV_RANDP_*), pass-stream kernels
     const bdpt_dev_lightpath* lp;
     const unsigned* sid;            // per pass
     const int* vlp;                 // per pass

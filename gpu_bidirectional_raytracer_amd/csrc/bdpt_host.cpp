@@ -37,6 +37,7 @@ static_assert(sizeof(bdpt_dev_lightpath) == sizeof(bdpt_lightpath), "VLP layout"
 static_assert(sizeof(bdpt_dev_vec) == sizeof(bdpt_vec), "colour layout");
 
 extern "C" __global__ void bdpt_mt607_kernel(const uint4*, unsigned, float*);
+extern "C" __global__ void bdpt_rand_planar_kernel(const float*, float*);
 extern "C" __global__ void bdpt_light_kernel(const bdpt_dev_sphere*, unsigned, const float*, int,
                                              bdpt_dev_lightpath*);
 extern "C" const void* bdpt_path_kernel_table[36];   // [(S > 1) * 18 + (BVH ? 17 : n <= 16 ? n : 0)]
@@ -114,6 +115,7 @@ struct bdpt_ctx {
     size_t rbuf_cap = 0;                // elements
     uint4* d_params = nullptr;          // 4096 x {matrix_a, mask_b, mask_c, seed}
     float* d_rand = nullptr;
+    float* d_rndp = nullptr;            // planar copy of d_rand (bdpt_rand_planar_kernel)
     bdpt_dev_lightpath* d_lp = nullptr;
     bdpt_dev_sphere* d_sph = nullptr;
     unsigned sph_cap = 0;
@@ -263,7 +265,7 @@ static int upload_scene(bdpt_ctx* c) {
 }
 
 static void release(bdpt_ctx* c) {
-    void* bufs[] = {c->d_params, c->d_rand, c->d_lp, c->d_sph, c->d_lights, c->d_geom, c->d_lightrec, c->d_colors,
+    void* bufs[] = {c->d_params, c->d_rand, c->d_rndp, c->d_lp, c->d_sph, c->d_lights, c->d_geom, c->d_lightrec, c->d_colors,
                     c->d_counter, c->d_pixels, c->d_thr, c->d_pass, c->d_rbuf, c->d_bvh_nodes,
                     c->d_bvh_geom, c->d_big_geom, c->d_mat, c->d_bvh_ids, c->d_big_ids,
                     c->d_fcolors, c->d_fcounter, c->d_fpixels, c->d_ftmp, c->d_ftmpc};
@@ -677,6 +679,7 @@ int bdpt_create(bdpt_ctx** out, const bdpt_sphere* spheres, unsigned n, int W, i
     const size_t np = (size_t)W * H;
     CK(hipMalloc(&c->d_params, sizeof(c->h_params)));
     CK(hipMalloc(&c->d_rand, sizeof(float) * BDPT_RAND_N));
+    CK(hipMalloc(&c->d_rndp, sizeof(float) * BDPT_DEV_RANDP_PLANES * BDPT_DEV_RANDP_PL));
     CK(hipMalloc(&c->d_lp, sizeof(bdpt_dev_lightpath) * BDPT_LIGHT_POINTS));
     CK(hipMalloc(&c->d_colors, sizeof(bdpt_dev_vec) * np));
     CK(hipMalloc(&c->d_counter, sizeof(unsigned) * np));
@@ -821,6 +824,9 @@ static int one_generate_rand(bdpt_ctx* c, unsigned seed) {
     hipLaunchKernelGGL(bdpt_mt607_kernel, dim3(BDPT_MT_RNG_COUNT / 64), dim3(64), 0, c->stream,
                        (const uint4*)c->d_params, seed, c->d_rand);
     HIPCHK(c, hipGetLastError());
+    hipLaunchKernelGGL(bdpt_rand_planar_kernel, dim3((BDPT_DEV_RANDP_PLANES * BDPT_DEV_RANDP_PL + 255) / 256),
+                       dim3(256), 0, c->stream, (const float*)c->d_rand, c->d_rndp);
+    HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->rand_ready = true;
     return BDPT_OK;
@@ -908,6 +914,7 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
     a.geom = c->d_geom;
     a.emis_mask = c->emis_mask;
     a.rnd = c->d_rand;
+    a.rndp = c->d_rndp;
     a.lp = c->d_lp;
     a.colors = c->d_colors;
     a.counter = c->d_counter;

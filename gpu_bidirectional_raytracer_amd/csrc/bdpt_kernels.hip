@@ -286,6 +286,20 @@ __device__ __forceinline__ void mt_step(unsigned (&mt)[19], unsigned a, unsigned
     if (k < BDPT_DEV_N_PER_RNG) out[tid + k * 4096] = ((float)y + 1.0f) / 4294967296.0f;
 }
 
+// Planar copy of d_Rand for the pass-stream path kernel: a lane reads d_Rand[j .. j+4] with
+// j = 26 + 25 i + 5 depth + sid, so neighbouring pixels are 25 entries apart -- in 25 planes by
+// j mod 25 they are adjacent (the 32 pixels of a workgroup row share one 128-B line per plane).
+// Planes 25..28 repeat planes 0..3 one entry on, so j + c (c <= 4) is plane (j mod 25) + c at
+// j / 25 without a wrap.
+extern "C" __global__ __launch_bounds__(256) void bdpt_rand_planar_kernel(const float* __restrict__ rnd,
+                                                                        float* __restrict__ rndp) {
+    const unsigned o = blockIdx.x * 256u + threadIdx.x;
+    if (o >= BDPT_DEV_RANDP_PLANES * BDPT_DEV_RANDP_PL) return;
+    const unsigned p = o / BDPT_DEV_RANDP_PL, q = o - p * BDPT_DEV_RANDP_PL;
+    const unsigned src = p < 25u ? 25u * q + p : 25u * (q + 1u) + (p - 25u);
+    rndp[o] = src < BDPT_DEV_RAND_N ? rnd[src] : 0.f;
+}
+
 template <int... S>
 __device__ __forceinline__ void mt_round(unsigned (&mt)[19], unsigned a, unsigned mb, unsigned mc,
                                          float* __restrict__ out, int tid, int k0,
@@ -427,6 +441,23 @@ __device__ __forceinline__ void load_rand5(const float* __restrict__ rnd, unsign
 #else
     q0 = rnd[j]; q1 = rnd[j + 1]; q2 = rnd[j + 2]; q3 = rnd[j + 3]; q4 = rnd[j + 4];
 #endif
+}
+
+#ifndef BDPT_RAND_PLANAR
+#define BDPT_RAND_PLANAR 1
+#endif
+// d_Rand[j .. j+4] from the planar copy: plane j mod 25 + c at j / 25, as buffer loads with the
+// plane offsets c * PL in the scalar offset (one address register for all five)
+__device__ __forceinline__ void load_rand5p(__amdgpu_buffer_rsrc_t rs, unsigned j, float& q0,
+                                            float& q1, float& q2, float& q3, float& q4) {
+    const unsigned qd = j / 25u, r = j - qd * 25u;
+    const unsigned vo = (r * BDPT_DEV_RANDP_PL + qd) * 4u;
+    constexpr unsigned P4 = BDPT_DEV_RANDP_PL * 4u;
+    q0 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, vo, 0, 0));
+    q1 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, vo, P4, 0));
+    q2 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, vo, 2 * P4, 0));
+    q3 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, vo, 3 * P4, 0));
+    q4 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, vo, 4 * P4, 0));
 }
 
 // f(S), f(S-1), ..., f(0) with compile-time indices while f returns true
@@ -718,6 +749,15 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
     unsigned depth = 0;
     unsigned j = (ibase + SID[0]) % M5;
     float q0, q1, q2, q3, q4;
+#if BDPT_RAND_PLANAR
+    // one pass per lane (pass streams, S = npass): the lanes of a wave stay on one sid and depth,
+    // so their gathers are adjacent in the planar copy (wave-uniform choice)
+    const bool planar = STREAMS && nslot == 1 && a.rndp != nullptr;
+    const __amdgpu_buffer_rsrc_t rsp = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)a.rndp, (short)0, (int)(BDPT_DEV_RANDP_PLANES * BDPT_DEV_RANDP_PL * 4u), 0x00020000);
+    if (planar) load_rand5p(rsp, j, q0, q1, q2, q3, q4);
+    else
+#endif
     load_rand5(rnd, j, q0, q1, q2, q3, q4);
     f3 ro = mk(0.f, 0.f, 0.f), rd = ro, thr = ro, rad = ro, nl = ro;
     bool specular = true, fresh = true;
@@ -1254,6 +1294,10 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                 asm volatile("" : "+v"(xyv));
                 const unsigned li = (xyv >> 16) * (unsigned)a.W + (xyv & 0xffffu);
                 j = (26u + li * 25u + depth * 5u + SID[k]) % M5;
+#if BDPT_RAND_PLANAR
+                if (planar) load_rand5p(rsp, j, q0, q1, q2, q3, q4);
+                else
+#endif
                 load_rand5(rnd, j, q0, q1, q2, q3, q4);
             }
         }
