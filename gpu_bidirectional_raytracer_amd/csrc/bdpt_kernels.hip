@@ -201,6 +201,9 @@ __device__ __forceinline__ troots roots_of(tdet q) {
 #ifndef BDPT_DET_SKIP
 #define BDPT_DET_SKIP 1
 #endif
+#ifndef BDPT_LAST_SKIP
+#define BDPT_LAST_SKIP 1
+#endif
 #ifndef BDPT_NEE_MARKSTEIN
 #define BDPT_NEE_MARKSTEIN 1
 #endif
@@ -908,6 +911,17 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                     // per lane, so the results are unchanged.
                     const bool isdiff = (mat & 255) == BDPT_DEV_DIFF;
                     const f3 cc = mk(cm.x, cm.y, cm.z);
+#if BDPT_LAST_SKIP
+                    // the path's last segment (depth 6, :621): the next direction and the
+                    // specular weights are never used -- a diffuse vertex still weights its NEE
+                    if (depth >= 6u) {
+                        if (isdiff) {
+                            specular = false;
+                            thr = mul(thr, cc);
+                            diff = true;
+                        }
+                    } else {
+#endif
                     f3 refl = rd;
                     bool refr = false, into = false;
                     float nnt = 0.f, ddn = 0.f, cos2t = 0.f;
@@ -966,6 +980,9 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                             rd = reflect ? refl : U;
                         }
                     }
+#if BDPT_LAST_SKIP
+                    }
+#endif
                     ro = hit;
                 }
 #else
