@@ -515,6 +515,32 @@ static hipFunction_t jit_path_kernel(bdpt_ctx* c, bool streams) {
     }
     if (nl == 0) lrec += "{0,0,0,0},{0,0,0,0}";
     lrec += "}";
+    // Zero-throughput exit (bdpt_kernels.hip BDPT_ZERO_EXIT) is exact when every later term a
+    // path could add is finite: the NEE term divides by len^2, len = distance from a vertex on a
+    // non-emitter sphere to a point on an emitter, so every emitter must keep a gap >= 1 from every
+    // other sphere's surface (then len stays far from 0 after rounding) and 4 pi r^2 be finite.
+    // Only compiled in when the scene has a black non-emitter (else it would only cost a test).
+    bool zero_exit = false;
+    for (unsigned i = 0; i < n; i++) {
+        const bdpt_sphere& o = c->spheres[i];
+        const bool emits = !(o.e.x == 0.f && o.e.y == 0.f && o.e.z == 0.f);
+        if (!emits && o.c.x == 0.f && o.c.y == 0.f && o.c.z == 0.f) zero_exit = true;
+    }
+    for (unsigned i = 0; i < n && zero_exit; i++) {
+        const bdpt_sphere& e = c->spheres[i];
+        if (e.e.x == 0.f && e.e.y == 0.f && e.e.z == 0.f) continue;
+        if (!(4.0 * 3.14159265358979 * (double)e.rad * e.rad < 1e30)) zero_exit = false;
+        for (unsigned k = 0; k < n && zero_exit; k++) {
+            if (k == i) continue;
+            const bdpt_sphere& o = c->spheres[k];
+            const double dx = (double)e.p.x - o.p.x, dy = (double)e.p.y - o.p.y, dz = (double)e.p.z - o.p.z;
+            const double d = sqrt(dx * dx + dy * dy + dz * dz);
+            double gap = d - e.rad - o.rad;                              // apart
+            if (o.rad - d - e.rad > gap) gap = o.rad - d - e.rad;        // emitter inside o
+            if (e.rad - d - o.rad > gap) gap = e.rad - d - o.rad;        // o inside the emitter
+            if (!(gap >= 1.0)) zero_exit = false;
+        }
+    }
     const char* wenv = getenv("BDPT_JIT_WAVES");
     int waves = wenv ? atoi(wenv) : 6;
     const std::string name = "&bdpt_path_kernel_t<" + std::to_string(n) + (streams ? ", true>" : ", false>");
@@ -527,6 +553,7 @@ static hipFunction_t jit_path_kernel(bdpt_ctx* c, bool streams) {
             "-fno-gpu-flush-denormals-to-zero", "-DBDPT_JIT=1", "-DBDPT_JIT_N=" + std::to_string(n),
             "-DBDPT_JIT_EMIS=" + std::to_string(emis) + "ull", "-DBDPT_JIT_GEOM=" + geom,
             "-DBDPT_JIT_NL=" + std::to_string(nl), "-DBDPT_JIT_LREC=" + lrec,
+            "-DBDPT_JIT_ZERO_SAFE=" + std::to_string(zero_exit ? 1 : 0),
             "-DBDPT_WAVES_PER_SIMD=" + std::to_string(waves)};
         std::vector<std::string> all = opts;
         if (const char* extra = getenv("BDPT_JIT_FLAGS")) {    // experiments: extra -D options

@@ -201,6 +201,9 @@ __device__ __forceinline__ troots roots_of(tdet q) {
 #ifndef BDPT_DET_SKIP
 #define BDPT_DET_SKIP 1
 #endif
+#ifndef BDPT_ZERO_EXIT
+#define BDPT_ZERO_EXIT 1
+#endif
 #ifndef BDPT_LAST_SKIP
 #define BDPT_LAST_SKIP 1
 #endif
@@ -614,7 +617,9 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
         for (int s = threadIdx.x; s < n; s += 256) {
             const bdpt_dev_sphere S = a.sph[s];
             const bool emis = !(S.ex == 0.f && S.ey == 0.f && S.ez == 0.f);
-            C[s] = make_float4(S.cx, S.cy, S.cz, __int_as_float(S.refl | (emis ? 256 : 0)));
+            // bit 8: emitter; bit 9: black non-emitter (c = 0: a hit zeroes the throughput)
+            const bool black = !emis && S.cx == 0.f && S.cy == 0.f && S.cz == 0.f;
+            C[s] = make_float4(S.cx, S.cy, S.cz, __int_as_float(S.refl | (emis ? 256 : 0) | (black ? 512 : 0)));
             E[s] = make_float4(S.ex, S.ey, S.ez, S.rad);
             P[s] = make_float4(S.px, S.py, S.pz, 0.f);
             G[s] = make_float4(S.px, S.py, S.pz, S.rr);
@@ -901,6 +906,15 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                         rad = add(rad, mul(thr, smul(fabsf(dp), mk(em.x, em.y, em.z))));
                     }
                     done = true;
+#if BDPT_ZERO_EXIT && defined(BDPT_JIT) && BDPT_JIT_ZERO_SAFE
+                } else if (N == BDPT_JIT_N && (mat & 512)) {
+                    // A black surface (cornell's front wall) makes the throughput exactly 0 (the
+                    // reference multiplies it by c = 0 whatever the material), so everything the
+                    // path adds from here on -- this vertex's NEE included -- is 0 * (finite) = +0:
+                    // the host proved the NEE term finite for this scene (every emitter keeps a gap
+                    // >= 1 from every other surface, bdpt_host.cpp).  rad is final: end the path.
+                    done = true;
+#endif
 #if BDPT_MERGE_REFR
                 } else {
                     // DIFF (:663-703), SPEC (:704-714), REFR (:715-770).  Nearly every wave holds

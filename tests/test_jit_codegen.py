@@ -59,3 +59,21 @@ def test_specialised_build_offline(scene):
     # saved exec masks and spilled 86 SGPRs into VGPR lanes; the lane-mask loop has none)
     assert streams[0]["sgpr_spill_count"] == 0, streams
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_zero_exit_rule():
+    """The black-surface path exit (bdpt_kernels.hip BDPT_ZERO_EXIT) is compiled in only for scenes
+    with a black non-emitter whose emitters keep a gap >= 1 from every other surface (the rule of
+    bdpt_host.cpp jit_path_kernel, mirrored by tools/jit_codegen_check.py)."""
+    import jit_codegen_check as jc
+    sys.path.insert(0, REPO)
+    import gpu_bidirectional_raytracer_amd as g
+    want = {"cornell": True, "cornell_glass": True, "mod_cornell": True,      # black front wall
+            "caustic": False, "simple": False, "cornell_multi": False, "open": False}   # nothing black
+    for scene, safe in want.items():
+        _, sp = g.read_scene(os.path.join(SCENES, scene + ".scn"))
+        assert jc.zero_exit_safe(sp) == safe, scene
+    # a light touching a black wall: no exit
+    _, sp = g.read_scene(os.path.join(SCENES, "cornell.scn"))
+    sp[8]["p"] = [50.0, 81.6 - 7.5, 81.6]
+    assert not jc.zero_exit_safe(sp)

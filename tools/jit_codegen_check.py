@@ -49,7 +49,31 @@ def jit_defines(spheres):
     if not lrec:
         lrec = ["{0,0,0,0}", "{0,0,0,0}"]
     return [f"-DBDPT_JIT_N={len(spheres)}", f"-DBDPT_JIT_EMIS={emis}ull", "-DBDPT_JIT_GEOM={" + ",".join(parts) + "}",
-            f"-DBDPT_JIT_NL={nl}", "-DBDPT_JIT_LREC={" + ",".join(lrec) + "}"]
+            f"-DBDPT_JIT_NL={nl}", "-DBDPT_JIT_LREC={" + ",".join(lrec) + "}",
+            f"-DBDPT_JIT_ZERO_SAFE={int(zero_exit_safe(spheres))}"]
+
+
+def zero_exit_safe(spheres):
+    """bdpt_host.cpp jit_path_kernel's test: some non-emitter is black, every emitter keeps a gap
+    >= 1 from every other sphere's surface and has a finite area."""
+    import math
+    if not any(not any(float(v) != 0.0 for v in o["e"]) and all(float(v) == 0.0 for v in o["c"])
+               for o in spheres):
+        return False
+    for i, e in enumerate(spheres):
+        if not any(float(v) != 0.0 for v in e["e"]):
+            continue
+        re = float(e["rad"])
+        if not 4.0 * math.pi * re * re < 1e30:
+            return False
+        for k, o in enumerate(spheres):
+            if k == i:
+                continue
+            ro = float(o["rad"])
+            d = math.dist([float(v) for v in e["p"]], [float(v) for v in o["p"]])
+            if not max(d - re - ro, ro - d - re, re - d - ro) >= 1.0:
+                return False
+    return True
 
 
 def scalar_writes(asm):
