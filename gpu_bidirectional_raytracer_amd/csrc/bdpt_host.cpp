@@ -515,21 +515,32 @@ static hipFunction_t jit_path_kernel(bdpt_ctx* c, bool streams) {
     }
     if (nl == 0) lrec += "{0,0,0,0},{0,0,0,0}";
     lrec += "}";
-    // Zero-throughput exit (bdpt_kernels.hip BDPT_ZERO_EXIT) is exact when every later term a
-    // path could add is finite: the NEE term divides by len^2, len = distance from a vertex on a
-    // non-emitter sphere to a point on an emitter, so every emitter must keep a gap >= 1 from every
-    // other sphere's surface (then len stays far from 0 after rounding) and 4 pi r^2 be finite.
-    // Only compiled in when the scene has a black non-emitter (else it would only cost a test).
-    bool zero_exit = false;
+    // Black-surface exit (bdpt_kernels.hip BDPT_ZERO_EXIT) is exact when the throughput before
+    // the black hit is finite (0 * thr = 0) and every later term a path could add is finite
+    // (0 * term = +0).  Scene values finite and colours <= 1e3: thr <= (4e3)^7 after 7 segments.
+    // Emission and VLP radiance <= e * 4 pi r^2 < 1e37.  The NEE term e * 4 pi r^2 * wi * wo / len^2
+    // needs len away from 0: every emitter keeps a gap >= max(1, 1e-4 * scene scale) from every
+    // other sphere's surface, far above the rounding of hit points (~2^-23 * scale).  Compiled in
+    // only when the scene has a black non-emitter (else it would only cost a test).
+    bool zero_exit = false, sane = true;
+    double scale = 0.0;
     for (unsigned i = 0; i < n; i++) {
         const bdpt_sphere& o = c->spheres[i];
+        const double v[10] = {o.rad, o.p.x, o.p.y, o.p.z, o.e.x, o.e.y, o.e.z, o.c.x, o.c.y, o.c.z};
+        for (double x : v) sane = sane && std::isfinite(x);
+        sane = sane && o.c.x <= 1e3f && o.c.y <= 1e3f && o.c.z <= 1e3f;
+        const double sc = sqrt((double)o.p.x * o.p.x + (double)o.p.y * o.p.y + (double)o.p.z * o.p.z) + fabs(o.rad);
+        if (sc > scale) scale = sc;
         const bool emits = !(o.e.x == 0.f && o.e.y == 0.f && o.e.z == 0.f);
         if (!emits && o.c.x == 0.f && o.c.y == 0.f && o.c.z == 0.f) zero_exit = true;
     }
+    zero_exit = zero_exit && sane;
+    const double min_gap = 1e-4 * scale > 1.0 ? 1e-4 * scale : 1.0;
     for (unsigned i = 0; i < n && zero_exit; i++) {
         const bdpt_sphere& e = c->spheres[i];
         if (e.e.x == 0.f && e.e.y == 0.f && e.e.z == 0.f) continue;
-        if (!(4.0 * 3.14159265358979 * (double)e.rad * e.rad < 1e30)) zero_exit = false;
+        const double emax = fmax(fabs(e.e.x), fmax(fabs(e.e.y), fabs(e.e.z)));
+        if (!(emax * 4.0 * 3.14159265358979 * (double)e.rad * e.rad < 1e37)) zero_exit = false;
         for (unsigned k = 0; k < n && zero_exit; k++) {
             if (k == i) continue;
             const bdpt_sphere& o = c->spheres[k];
@@ -538,7 +549,7 @@ static hipFunction_t jit_path_kernel(bdpt_ctx* c, bool streams) {
             double gap = d - e.rad - o.rad;                              // apart
             if (o.rad - d - e.rad > gap) gap = o.rad - d - e.rad;        // emitter inside o
             if (e.rad - d - o.rad > gap) gap = e.rad - d - o.rad;        // o inside the emitter
-            if (!(gap >= 1.0)) zero_exit = false;
+            if (!(gap >= min_gap)) zero_exit = false;
         }
     }
     const char* wenv = getenv("BDPT_JIT_WAVES");

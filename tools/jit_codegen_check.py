@@ -54,24 +54,30 @@ def jit_defines(spheres):
 
 
 def zero_exit_safe(spheres):
-    """bdpt_host.cpp jit_path_kernel's test: some non-emitter is black, every emitter keeps a gap
-    >= 1 from every other sphere's surface and has a finite area."""
+    """bdpt_host.cpp jit_path_kernel's rule: some non-emitter is black, all scene values are finite
+    and colours <= 1e3, every emitter has e * 4 pi r^2 < 1e37 and keeps a gap >= max(1, 1e-4 *
+    scene scale) from every other sphere's surface."""
     import math
+    vals = [float(v) for o in spheres for v in (o["rad"], *o["p"], *o["e"], *o["c"])]
+    if not all(math.isfinite(v) for v in vals) or any(float(v) > 1e3 for o in spheres for v in o["c"]):
+        return False
     if not any(not any(float(v) != 0.0 for v in o["e"]) and all(float(v) == 0.0 for v in o["c"])
                for o in spheres):
         return False
+    scale = max(math.hypot(*[float(v) for v in o["p"]]) + abs(float(o["rad"])) for o in spheres)
+    min_gap = max(1.0, 1e-4 * scale)
     for i, e in enumerate(spheres):
         if not any(float(v) != 0.0 for v in e["e"]):
             continue
         re = float(e["rad"])
-        if not 4.0 * math.pi * re * re < 1e30:
+        if not max(abs(float(v)) for v in e["e"]) * 4.0 * math.pi * re * re < 1e37:
             return False
         for k, o in enumerate(spheres):
             if k == i:
                 continue
             ro = float(o["rad"])
             d = math.dist([float(v) for v in e["p"]], [float(v) for v in o["p"]])
-            if not max(d - re - ro, ro - d - re, re - d - ro) >= 1.0:
+            if not max(d - re - ro, ro - d - re, re - d - ro) >= min_gap:
                 return False
     return True
 
