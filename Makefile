@@ -48,7 +48,10 @@ $(BUILD)/bdpt_cpu.o: $(CSRC)/bdpt_cpu.cpp $(CSRC)/bdpt_cpu.h include/bdpt.h | $(
 $(BUILD)/bdpt_util.o: $(CSRC)/bdpt_util.c include/bdpt.h | $(BUILD)
 	$(CC) $(CFLAGS) -c $< -o $@
 
-$(LIB): $(BUILD)/bdpt_kernels.o $(BUILD)/bdpt_host.o $(BUILD)/bdpt_bvh.o $(BUILD)/bdpt_cpu.o $(BUILD)/bdpt_util.o
+$(BUILD)/bdpt_ckpt.o: $(CSRC)/bdpt_ckpt.c include/bdpt.h | $(BUILD)
+	$(CC) $(CFLAGS) -c $< -o $@
+
+$(LIB): $(BUILD)/bdpt_kernels.o $(BUILD)/bdpt_host.o $(BUILD)/bdpt_bvh.o $(BUILD)/bdpt_cpu.o $(BUILD)/bdpt_util.o $(BUILD)/bdpt_ckpt.o
 	mkdir -p $(dir $(LIB))
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lm -ldl
 
@@ -80,10 +83,10 @@ $(ASAN_DIR)/asan_cpu_abi.o: tests/native/asan_cpu_abi.cpp $(CSRC)/bdpt_cpu.h inc
 $(ASAN_DIR)/bdpt_oracle.o: oracle/bdpt_oracle.c include/bdpt.h | $(ASAN_DIR)
 	$(CC) $(ASAN_FLAGS) -std=gnu11 -c $< -o $@
 
-$(ASAN_DIR)/smallpt_asan: $(ASAN_DIR)/smallpt.o $(ASAN_DIR)/bdpt_util.o $(ASAN_DIR)/bdpt_cpu.o $(ASAN_DIR)/asan_cpu_abi.o
+$(ASAN_DIR)/smallpt_asan: $(ASAN_DIR)/smallpt.o $(ASAN_DIR)/bdpt_util.o $(ASAN_DIR)/bdpt_ckpt.o $(ASAN_DIR)/bdpt_cpu.o $(ASAN_DIR)/asan_cpu_abi.o
 	g++ $(ASAN_FLAGS) -o $@ $^ -lm -pthread
 
-$(ASAN_DIR)/oracle_asan: tests/native/oracle_asan.c $(ASAN_DIR)/bdpt_oracle.o $(ASAN_DIR)/bdpt_util.o $(ASAN_DIR)/bdpt_cpu.o $(ASAN_DIR)/asan_cpu_abi.o
+$(ASAN_DIR)/oracle_asan: tests/native/oracle_asan.c $(ASAN_DIR)/bdpt_oracle.o $(ASAN_DIR)/bdpt_util.o $(ASAN_DIR)/bdpt_ckpt.o $(ASAN_DIR)/bdpt_cpu.o $(ASAN_DIR)/asan_cpu_abi.o
 	g++ $(ASAN_FLAGS) -x c -std=gnu11 -c $< -o $(ASAN_DIR)/oracle_asan_main.o
 	g++ $(ASAN_FLAGS) -o $@ $(ASAN_DIR)/oracle_asan_main.o $(filter %.o,$^) -lm -pthread
 

@@ -142,9 +142,176 @@ def cpu_baseline(sp, cam, W, H, rows, sid, vlp, seconds):
             "node_linear_estimate_note": "1-core rate x nproc: an upper bound for the whole host (perfect scaling)"}
 
 
+def resolve_launch(gpus, env, visible=None, fixed_bands=0, devices=None):
+    """How `--gpus N` runs (the driver's contract): under torchrun (WORLD_SIZE set) one rank per
+    GPU and WORLD_SIZE must equal N; without it, N = 1 is one context on device 0 and N > 1 one
+    in-process multi-device context (bdpt_create_multi: pixel bands over devices 0..N-1, the frame
+    assembled by an in-process RCCL reduce).  Returns (mode, world, rank, local); raises
+    SystemExit (non-zero) on any mismatch."""
+    if gpus < 1:
+        raise SystemExit(f"bench.py: --gpus must be >= 1 (got {gpus})")
+    if env.get("WORLD_SIZE") is not None:
+        world = int(env["WORLD_SIZE"])
+        if world != gpus:
+            raise SystemExit(f"bench.py: --gpus {gpus} but torchrun started WORLD_SIZE={world} ranks; "
+                             "launch one rank per GPU (--nproc-per-node N with --gpus N)")
+        return "ranks", world, int(env.get("RANK", "0")), int(env.get("LOCAL_RANK", "0"))
+    if devices is not None:                                   # explicit device list (rehearsal)
+        if len(devices) != gpus or min(devices) < 0 or (visible is not None and max(devices) >= visible):
+            raise SystemExit(f"bench.py: --devices {devices} does not name {gpus} visible GPU(s)")
+    elif gpus == 1:
+        return "single", 1, 0, 0
+    elif visible is not None and gpus > visible:
+        raise SystemExit(f"bench.py: --gpus {gpus} but only {visible} GPU(s) are visible")
+    if fixed_bands and fixed_bands % gpus:
+        raise SystemExit(f"bench.py: this workload has {fixed_bands} fixed bands; --gpus must divide it")
+    return "inproc", 1, 0, 0
+
+
+def _read(path):
+    try:
+        with open(path) as f:
+            return f.read().strip()
+    except OSError:
+        return None
+
+
+def gpu_identity(device):
+    """Which GPU this is: name / arch / CUs / memory from the runtime, and from sysfs (by PCI
+    address) its unique id, serial, sclk / mclk levels (current marked), power cap -- so a
+    measurement can be placed within the box-to-box spread."""
+    import torch
+    p = torch.cuda.get_device_properties(device)
+    ident = {"name": p.name, "arch": getattr(p, "gcnArchName", None),
+             "cus": p.multi_processor_count, "memory_gib": round(p.total_memory / 2 ** 30, 1)}
+    dom, bus, dev = (getattr(p, "pci_domain_id", None), getattr(p, "pci_bus_id", None),
+                     getattr(p, "pci_device_id", None))
+    if bus is not None:
+        addr = f"{dom or 0:04x}:{bus:02x}:{dev or 0:02x}.0"
+        ident["pci"] = addr
+        d = f"/sys/bus/pci/devices/{addr}"
+        for key, fn in (("unique_id", "unique_id"), ("serial", "serial_number"), ("product", "product_name"),
+                        ("vbios", "vbios_version")):
+            v = _read(os.path.join(d, fn))
+            if v:
+                ident[key] = v
+        for key, fn in (("sclk", "pp_dpm_sclk"), ("mclk", "pp_dpm_mclk")):
+            v = _read(os.path.join(d, fn))
+            if v:
+                lines = [l.split(":", 1)[1].strip() for l in v.splitlines() if ":" in l]
+                cur = [l.split(":", 1)[1].replace("*", "").strip() for l in v.splitlines() if "*" in l]
+                ident[key] = {"levels": lines, "current": cur[0] if cur else None}
+        try:
+            for hw in sorted(os.listdir(os.path.join(d, "hwmon"))):
+                cap = _read(os.path.join(d, "hwmon", hw, "power1_cap"))
+                cmax = _read(os.path.join(d, "hwmon", hw, "power1_cap_max"))
+                if cap:
+                    ident["power_cap_w"] = round(int(cap) / 1e6, 1)
+                if cmax:
+                    ident["power_cap_max_w"] = round(int(cmax) / 1e6, 1)
+        except OSError:
+            pass
+    return ident
+
+
+def cpu_topology():
+    """{cpu: (package, core)} for every online CPU, from sysfs."""
+    topo = {}
+    for c in range(os.cpu_count() or 1):
+        base = f"/sys/devices/system/cpu/cpu{c}/topology"
+        pk, co = _read(os.path.join(base, "physical_package_id")), _read(os.path.join(base, "core_id"))
+        if pk is not None and co is not None:
+            topo[c] = (int(pk), int(co))
+    return topo
+
+
+def cpu_probe(spec):
+    """Child process of cpu_baseline: pin to spec['cpus'], run the oracle with spec['threads']
+    threads over a bounded region for about spec['seconds'], print the rate (Msamples/s)."""
+    os.sched_setaffinity(0, spec["cpus"])
+    import numpy as np
+    import oracle
+    import gpu_bidirectional_raytracer_amd as g
+    W, H = spec["W"], spec["H"]
+    cam, sp = g.read_scene(os.path.join(REPO, "assets", "scenes", spec["scene"] + ".scn"))
+    g.update_camera(cam, W, H)
+    rnd = oracle.mt607(0)
+    lp = oracle.light_pass(sp, rnd, 0)
+    sid, vlp = np.array(spec["sid"], np.uint32), np.array(spec["vlp"], np.int32)
+    y0, th = spec["y0"], spec["threads"]
+    oracle.path_passes(sp, rnd, cam, W, H, lp, sid[:1], vlp[:1], rows=(y0, y0 + 2), nthreads=th)   # warm
+    rows = spec.get("rows")
+    if not rows:                                              # calibrate: rows for ~`seconds`
+        t = time.perf_counter()
+        oracle.path_passes(sp, rnd, cam, W, H, lp, sid[:1], vlp[:1], rows=(y0, y0 + 8), nthreads=th)
+        rate = 8 * W / max(time.perf_counter() - t, 1e-4)
+        rows = max(8, min(H - y0, int(rate * spec["seconds"] / W)))
+    t = time.perf_counter()
+    oracle.path_passes(sp, rnd, cam, W, H, lp, sid[:1], vlp[:1], rows=(y0, y0 + rows), nthreads=th)
+    dt = time.perf_counter() - t
+    print(json.dumps({"value": rows * W / dt / 1e6, "rows": rows, "seconds": dt}), flush=True)
+
+
+def smt_yield(scene, W, H, y0, sid, vlp, seconds, usable):
+    """Within this job's CPUs: k physical cores with one oracle thread each vs the same k cores
+    with both SMT siblings busy (2k threads).  Returns None when the affinity mask holds no core
+    with two siblings.  Runs in child processes pinned with sched_setaffinity (OpenMP threads
+    inherit the mask)."""
+    import subprocess
+    topo = cpu_topology()
+    try:
+        aff = sorted(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return None
+    cores = {}
+    for c in aff:
+        if c in topo:
+            cores.setdefault(topo[c], []).append(c)
+    pairs = [sorted(v)[:2] for v in cores.values() if len(v) >= 2]
+    k = min(len(pairs), max(1, usable // 2))
+    if k < 1:
+        return None
+    pairs = pairs[:k]
+    res, rows = {}, None
+    for label, cpus in (("one_thread_per_core", [p[0] for p in pairs]), ("two_threads_per_core", [c for p in pairs for c in p])):
+        spec = {"cpus": cpus, "threads": len(cpus), "scene": scene, "W": W, "H": H, "y0": y0, "rows": rows,
+                "sid": [int(x) for x in sid[:1]], "vlp": [int(x) for x in vlp[:1]], "seconds": seconds}
+        out = subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-probe", json.dumps(spec)],
+                             capture_output=True, text=True, timeout=600, env=dict(os.environ, OMP_NUM_THREADS=str(len(cpus))))
+        lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+        if out.returncode != 0 or not lines:
+            return {"error": (out.stderr or "")[-300:]}
+        d = json.loads(lines[-1])
+        res[label] = round(d["value"], 4)
+        rows = d["rows"]                                      # the same region for both runs
+    y = res["two_threads_per_core"] / res["one_thread_per_core"]
+    return {"cores_probed": k, "rows": [y0, y0 + rows], "rate_one_thread_per_core": res["one_thread_per_core"],
+            "rate_two_threads_per_core": res["two_threads_per_core"], "smt_yield": round(y, 3),
+            "node_physical_cores": len(set(topo.values())) or None}
+
+
+def _pmc_record(name, workload, scene, W, H, passes_per_launch, streams, specialized):
+    """The PMC record of profiles/<name> for this exact configuration (files hold one record per
+    workload), or None."""
+    path = os.path.join(REPO, "profiles", name)
+    if not os.path.exists(path):
+        return None
+    data = json.load(open(path))
+    recs = data.values() if isinstance(data, dict) and "scene" not in data else [data]
+    for rec in recs:
+        if rec.get("workload", "cornell1080") == workload and rec.get("scene") == scene \
+                and rec.get("width") == W and rec.get("height") == H \
+                and float(rec.get("passes_per_launch", -1)) == float(passes_per_launch) \
+                and rec.get("pass_streams") == streams and bool(rec.get("specialized", False)) == bool(specialized):
+            return rec
+    return None
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs of this job: under torchrun = WORLD_SIZE (one rank per GPU); without it, "
+                         "N > 1 renders on devices 0..N-1 through one in-process multi-device context")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="cornell1080", choices=sorted(WORKLOADS))
@@ -160,24 +327,35 @@ def main():
                     help="scene-specialised kernels (run-time compiled; results identical)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-smt-probe", action="store_true", help="skip the SMT-yield probe of the CPU baseline")
     ap.add_argument("--rehearse", action="store_true",
                     help="multi-rank dry run on fewer GPUs: gloo, ranks share devices (not a measurement)")
+    ap.add_argument("--devices", default=None,
+                    help="in-process multi-device run on these devices, e.g. 0,0 (rehearsal of --gpus 2 on one GPU)")
+    ap.add_argument("--cpu-probe", default=None, help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.cpu_probe:                                        # child of cpu_baseline: no GPU
+        return cpu_probe(json.loads(args.cpu_probe))
     wl = dict(WORKLOADS[args.workload])
     for k in ("scene", "width", "height", "passes", "band_rows"):
         if getattr(args, k) is not None:
             wl[k] = getattr(args, k)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    import torch
+    import torch                                              # device_count() does not initialise HIP
+    visible = torch.cuda.device_count()
+    dev_list = [int(x) for x in args.devices.split(",")] if args.devices else None
+    mode, world, rank, local = resolve_launch(args.gpus, os.environ, visible, wl["fixed_bands"], dev_list)
+    if mode == "single" and visible < 1:
+        raise SystemExit("bench.py: no GPU visible")
+    ndev = args.gpus if mode == "inproc" else 1               # devices of this process
 
     import gpu_bidirectional_raytracer_amd as g
     from gpu_bidirectional_raytracer_amd import sharding as shd
 
     if args.rehearse:
-        local = local % max(torch.cuda.device_count(), 1)
+        local = local % max(visible, 1)
+    if mode == "inproc":
+        local = (dev_list or [0])[0]
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
@@ -189,24 +367,33 @@ def main():
 
     W, H = wl["width"] + 1, wl["height"] + 1                 # smallpt_cpu.c:409-410
     band = wl["band_rows"]
-    nshards = wl["fixed_bands"] or world                     # weak64: 8 fixed bands, rank r renders band r
-    if world > nshards:
-        raise SystemExit(f"workload {args.workload} has {nshards} bands: at most {nshards} ranks")
+    units = world * ndev                                      # GPUs rendering the job
+    nshards = wl["fixed_bands"] or units                      # weak64: 8 fixed bands, GPU r renders band r
+    if units > nshards:
+        raise SystemExit(f"workload {args.workload} has {nshards} bands: at most {nshards} GPUs")
     cam, sp = g.read_scene(os.path.join(REPO, "assets", "scenes", wl["scene"] + ".scn"))
     g.update_camera(cam, W, H)
-    r = g.Renderer(sp, W, H, cam, device=local)
-    r.set_shard(rank, nshards, band)
+    if mode == "inproc":
+        devices = dev_list or list(range(ndev))
+        r = g.Renderer(sp, W, H, cam, devices=devices)
+        # device k of the group renders shard k of nshards (bdpt_set_shard on a group of ndev
+        # devices as shard 0 of nshards / ndev groups)
+        r.set_shard(0, nshards // ndev, band)
+    else:
+        devices = [local]
+        r = g.Renderer(sp, W, H, cam, device=local)
+        r.set_shard(rank, nshards, band)
     r.set_traversal(args.traversal)
     r.set_streams(args.streams)
     r.set_specialize(bool(args.specialize))
     r.light_pass(0)                                           # UpdateRendering2
     sched = g.PassScheduler()
     sched.light()
-    per_step = wl["passes"] * (world if (wl["scaling"] == "weak" and not wl["fixed_bands"]) else 1)
+    per_step = wl["passes"] * (units if (wl["scaling"] == "weak" and not wl["fixed_bands"]) else 1)
     sid, vlp = sched.next(per_step * (args.warmup + args.steps))
-    # samples per step over the whole job: every owned pixel of every rank, once per pass
-    job_pixels = sum(shd.owned_pixels(W, H, q, nshards, band) for q in range(world))
-    own_pixels = shd.owned_pixels(W, H, rank, nshards, band)
+    # samples per step over the whole job: every owned pixel of every GPU, once per pass
+    job_pixels = sum(shd.owned_pixels(W, H, q, nshards, band) for q in range(units))
+    own_pixels = shd.owned_pixels(W, H, rank, nshards, band)  # this rank's (or device 0's) share
 
     def step(k):
         a, b = k * per_step, (k + 1) * per_step
@@ -220,6 +407,7 @@ def main():
         step(k)
     r.synchronize()
     r.path_timing(reset=True)
+    r.kernel_timing(reset=True)
 
     # RCCL reduce target: torch tensors over the library's own device buffers (no copy)
     t_col = t_cnt = None
@@ -234,6 +422,8 @@ def main():
     r.synchronize()
     if dist is not None:                                      # assemble the frame on rank 0
         shd.reduce_frame(t_col, t_cnt, dst=0)
+    elif mode == "inproc":                                    # in-process RCCL reduce to device 0
+        r.reduce_frame()
     torch.cuda.synchronize()
     barrier()
     dt = time.perf_counter() - t0
@@ -242,20 +432,33 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
 
-    kern_ms, _ = r.kernel_timing()                            # path kernels alone
-    dev_ms, launches = r.path_timing()                        # + the pass-stream fold
+    kern_ms, launches = r.kernel_timing()                     # path kernels alone
+    dev_ms, _ = r.path_timing()                               # + the pass-stream fold
     samples = job_pixels * per_step * args.steps
     value = samples / dt / 1e6
+    ident = gpu_identity(local)
+    idents = [ident]
+    if dist is not None:
+        gathered = [None] * world
+        dist.all_gather_object(gathered, ident)
+        idents = gathered
+    elif mode == "inproc":
+        idents = [gpu_identity(d) for d in devices]
 
     if rank == 0:
-        if dist is not None:
-            r.update_pixels()
-            cnt = t_cnt.cpu().numpy().reshape(H, W)
-            owned = (torch.arange(H).numpy() // band) % nshards < world
-            assert (cnt[owned] == per_step * (args.warmup + args.steps)).all(), "reduced counters wrong"
+        spp_total = per_step * (args.warmup + args.steps)
+        if dist is not None or mode == "inproc":              # check the assembled frame's counters
+            if dist is not None:
+                r.update_pixels()
+                cnt = t_cnt.cpu().numpy().reshape(H, W)
+            else:
+                cnt = r.read_radiance()[1]
+            owned = (torch.arange(H).numpy() // band) % nshards < units
+            assert (cnt[owned] == spp_total).all() and (cnt[~owned] == 0).all(), "assembled counters wrong"
         w = WORK.get(wl["scene"])
         avg_launch_s = kern_ms / 1e3 / max(launches, 1)
         passes_per_launch = per_step * args.steps / max(launches, 1)
+        features = r.last_features
         roofline = None
         if w is not None:
             samples_per_launch = own_pixels * passes_per_launch
@@ -267,20 +470,17 @@ def main():
                 bytes_per_launch = own_pixels * ACCUM_BYTES_PER_PIXEL + samples_per_launch * 4 * w["rng_reads"]
             gbs = bytes_per_launch / avg_launch_s / 1e9
             fl = flop_per_sample(w) * samples_per_launch / avg_launch_s / 1e12
-            traffic = None
-            pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
-            if os.path.exists(pmc) and world == 1:
-                rec = json.load(open(pmc))
-                if rec.get("workload", "cornell1080") == args.workload and rec.get("scene") == wl["scene"] \
-                        and rec.get("passes_per_launch") == passes_per_launch \
-                        and rec.get("pass_streams") in (None, r.last_streams) \
-                        and rec.get("specialized", False) == r.last_specialized \
-                        and rec.get("width") == W and rec.get("height") == H:
-                    traffic = rec.get("hbm_bytes_per_launch")
+            single = world == 1 and ndev == 1
+            trec = _pmc_record("pmc_traffic.json", args.workload, wl["scene"], W, H, passes_per_launch,
+                               r.last_streams, r.last_specialized) if single else None
+            skips = [f for f in features if f in ("det_skip", "zero_exit", "last_skip", "bvh")]
             roofline = {"bound": "valu", "achieved": round(fl, 3), "peak": FP32_NOFMA_TFLOPS, "unit": "TFLOP/s",
-                        "frac": round(fl / FP32_NOFMA_TFLOPS, 4), "traffic": traffic,
+                        "frac": round(fl / FP32_NOFMA_TFLOPS, 4),
+                        "traffic": trec.get("hbm_bytes_per_launch") if trec else None,
                         "peak_fma": FP32_PEAK_TFLOPS, "frac_fma": round(fl / FP32_PEAK_TFLOPS, 4),
                         "flop_per_sample": round(flop_per_sample(w), 1),
+                        "flop_model": "reference-equivalent" if skips else "reference",
+                        "kernel_features": features,
                         "samples_per_launch": int(samples_per_launch),
                         "avg_launch_ms": round(avg_launch_s * 1e3, 4), "launches": launches,
                         "hbm": {"achieved": round(gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -288,24 +488,44 @@ def main():
                         "note": "fp32 VALU bound: -ffp-contract=off, so one add or mul per lane-cycle (78.6 T/s); "
                                 "FLOP model and per-sample bytes in DESIGN.md; traffic = calibrated PMC "
                                 "FETCH_SIZE+WRITE_SIZE per launch (profiles/pmc_traffic.json)"}
-            pv = os.path.join(REPO, "profiles", "pmc_valu.json")
-            if os.path.exists(pv) and world == 1:
-                rec = json.load(open(pv))
-                if rec.get("scene") == wl["scene"] and rec.get("passes_per_launch") == passes_per_launch \
-                        and rec.get("pass_streams") == r.last_streams and rec.get("width") == W \
-                        and rec.get("specialized", False) == r.last_specialized:
-                    roofline["valu_busy_pmc"] = rec["valu_busy"]
-                    roofline["lane_utilisation_pmc"] = rec["valu_lane_utilisation"]
-            if r.last_traversal == "bvh":
-                roofline["note"] = ("reference-equivalent FLOPs: the reference tests every sphere; the BVH "
-                                    "skips most tests, so this is work avoided, not VALU throughput")
+            if skips:
+                roofline["note"] += ("; achieved counts REFERENCE-EQUIVALENT FLOPs: the model prices the "
+                                     "reference's every-sphere, every-segment work, and this kernel provably skips "
+                                     f"some of it ({', '.join(skips)}: results unchanged), so frac measures "
+                                     "work delivered, not VALU efficiency -- see valu_busy_pmc")
+            vrec = _pmc_record("pmc_valu.json", args.workload, wl["scene"], W, H, passes_per_launch,
+                               r.last_streams, r.last_specialized) if single else None
+            if vrec:
+                for k in ("valu_busy", "valu_lane_utilisation", "wait_frac", "issue_stall_frac", "active_frac",
+                          "valu_insts_per_wave", "l2_hit_rate"):
+                    if k in vrec:
+                        roofline[{"valu_busy": "valu_busy_pmc",
+                                  "valu_lane_utilisation": "lane_utilisation_pmc"}.get(k, k + "_pmc")] = vrec[k]
         cpu = None
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and ndev == 1 and not args.no_cpu_baseline:
             rows = shd.owned_row_ranges(H, rank, nshards, band)
             region = (rows[0][0], rows[0][1]) if wl["fixed_bands"] else (0, H)
             cpu = cpu_baseline(sp, cam, W, H, region, sid, vlp, args.cpu_seconds)
+            if not args.no_smt_probe:
+                mid = region[0] + (region[1] - region[0]) // 3
+                smt = smt_yield(wl["scene"], W, H, mid, sid, vlp, max(2.0, args.cpu_seconds / 4), cpu["cores"])
+                cpu["smt"] = smt
+                if smt and smt.get("smt_yield") and smt.get("node_physical_cores"):
+                    # the verdict's node model: physical cores x 1-core rate x SMT yield
+                    cpu["node_estimate"] = round(smt["node_physical_cores"] * cpu["value_1core"] * smt["smt_yield"], 2)
+                    cpu["node_estimate_note"] = ("physical cores of the node x the 1-core rate (value_1core, same "
+                                                 "frame) x the SMT yield (k cores with both siblings busy / the "
+                                                 "same k cores with one thread each, same rows); assumes every "
+                                                 "core keeps the 1-core rate (no memory-bandwidth limit), so it "
+                                                 "is still an upper estimate of the whole host")
+        if mode == "ranks":
+            reduce_backend = "gloo (torch.distributed, host-staged)" if args.rehearse else "rccl (torch.distributed nccl)"
+        elif mode == "inproc":
+            reduce_backend = r.reduce_backend + " (in-process bdpt_create_multi)"
+        else:
+            reduce_backend = "none"
         line = {
-            "metric": METRIC, "value": round(value, 2), "unit": "Msamples/s", "n_gpus": world,
+            "metric": METRIC, "value": round(value, 2), "unit": "Msamples/s", "n_gpus": units,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": wl["scaling"], "vs_baseline": None, "dtype": "fp32",
             "data": f"synthetic: reference {wl['scene']}.scn + MT607 table (seed 0) + glibc-rand pass offsets",
@@ -314,25 +534,34 @@ def main():
                                    f"per diffuse vertex; {wl['config']}",
                        "scene": wl["scene"], "width": W, "height": H, "passes_per_step": per_step,
                        "samples_per_step": job_pixels * per_step,
-                       "spp_total": per_step * (args.warmup + args.steps),
-                       "parallelism": (f"{nshards} fixed {band}-row bands, rank r renders band r" if wl["fixed_bands"]
-                                       else f"pixel bands x{world} ({band}-row, interleaved)"),
+                       "spp_total": spp_total,
+                       "parallelism": (f"{nshards} fixed {band}-row bands, GPU r renders band r" if wl["fixed_bands"]
+                                       else f"pixel bands x{units} ({band}-row, interleaved)"),
+                       "launch": {"single": "one process, one GPU", "ranks": f"torchrun: {world} ranks, one GPU each",
+                                  "inproc": f"one process, multi-device context over {ndev} GPUs"}[mode],
                        "pass_streams": r.last_streams, "traversal": r.last_traversal,
                        "specialized": r.last_specialized},
+            "rccl_ranks": world if mode == "ranks" else (ndev if r.reduce_backend == "rccl" else 0),
+            "reduce_backend": reduce_backend,
+            "devices": [{"rank": q, **idents[q]} for q in range(len(idents))] if mode == "ranks"
+            else [{"device": d, **idents[i]} for i, d in enumerate(devices)],
             "device_ms_per_step": round(dev_ms / args.steps, 3),
             "roofline": roofline, "cpu_baseline": cpu,
-            "host": {"gpu": torch.cuda.get_device_name(local), "hostname": socket.gethostname()},
+            "host": {"gpu": ident.get("name"), "hostname": socket.gethostname(), "gpu_pci": ident.get("pci"),
+                     "gpu_unique_id": ident.get("unique_id")},
         }
         if cpu:
             line["speedup_vs_cpu"] = round(value / cpu["value"], 1)
             line["speedup_vs_cpu_node_linear_estimate"] = round(value / cpu["node_linear_estimate"], 1)
+            if cpu.get("node_estimate"):
+                line["speedup_vs_cpu_node_estimate"] = round(value / cpu["node_estimate"], 1)
+                line["north_star_100x_at_node_level"] = value / cpu["node_estimate"] >= 100.0
         if args.rehearse:
             line["rehearsal"] = "ranks share GPUs over gloo: exercises the multi-rank flow, not a measurement"
         print(json.dumps(line), flush=True)
     r.close()
     if dist is not None:
         dist.destroy_process_group()
-
 
 if __name__ == "__main__":
     main()

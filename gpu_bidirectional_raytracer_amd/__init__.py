@@ -17,7 +17,7 @@ from typing import Optional, Sequence, Tuple
 
 import numpy as np
 
-from ._lib import (BDPT_OK, COUNTER_CAP, DEFAULT_DAT, DIFF, KEY_DOWN, KEY_LEFT, KEY_PAGE_DOWN,
+from ._lib import (BDPT_OK, COUNTER_CAP, DEFAULT_DAT, DIFF, FEATURES, KEY_DOWN, KEY_LEFT, KEY_PAGE_DOWN,
                    KEY_PAGE_UP, KEY_RIGHT, KEY_UP, LIGHT_POINTS, LITE, RAND_N, REFR, SCENE_DIR, SPEC,
                    BdptError, Camera, LightPath, PassState, RandState, Sphere, Vec, lib)
 
@@ -249,6 +249,12 @@ class Renderer:
         return {1: "brute", 2: "bvh"}[int(lib.bdpt_last_traversal(self._h))]
 
     @property
+    def last_features(self) -> list:
+        """What the last path-pass kernel compiled in (include/bdpt.h BDPT_FEAT_*), by name."""
+        bits = int(lib.bdpt_last_kernel_features(self._h))
+        return [name for bit, name in sorted(FEATURES.items()) if bits & bit]
+
+    @property
     def num_devices(self) -> int:
         return int(lib.bdpt_num_devices(self._h))
 
@@ -335,6 +341,29 @@ class Renderer:
         lp = np.empty(LIGHT_POINTS, LIGHTPATH_DTYPE)
         self._chk(lib.bdpt_read_lightpaths(self._h, _ptr(lp)))
         return lp
+
+    def write_lightpaths(self, lp: np.ndarray) -> None:
+        lp = np.ascontiguousarray(lp, LIGHTPATH_DTYPE)
+        assert lp.shape == (LIGHT_POINTS,)
+        self._chk(lib.bdpt_write_lightpaths(self._h, _ptr(lp)))
+
+    def rand_seed(self) -> Optional[int]:
+        """Seed of the current MT607 table (None before the first light pass)."""
+        s = ctypes.c_uint()
+        return int(s.value) if lib.bdpt_rand_seed(self._h, ctypes.byref(s)) == BDPT_OK else None
+
+    def get_camera(self) -> Optional[Camera]:
+        cam = Camera()
+        return cam if lib.bdpt_get_camera(self._h, ctypes.byref(cam)) == BDPT_OK else None
+
+    def get_scene(self) -> np.ndarray:
+        n = lib.bdpt_get_scene(self._h, None, 0)
+        if n < 0:
+            raise BdptError(n, lib.bdpt_last_error(self._h).decode())
+        arr = np.zeros(n, SPHERE_DTYPE)
+        if n:
+            lib.bdpt_get_scene(self._h, _sphere_ptr(arr), n)
+        return arr
 
     def device_buffers(self) -> Tuple[int, int, int]:
         c, n, p = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
@@ -459,8 +488,16 @@ class SmallPT:
         self.renderer.save_checkpoint(path, blob)
 
     def LoadCheckpoint(self, path: str) -> None:
-        """Restore what SaveCheckpoint wrote; rendering continues bit for bit."""
+        """Restore what SaveCheckpoint wrote; rendering continues bit for bit.  The checkpoint
+        carries the render state too (camera, spheres, MT table seed, VLPs -- keys may have
+        edited them before the save): the context restores it, and the mirror takes over the
+        camera and spheres, so later keys continue from the saved state."""
         v = self._STATE.unpack(self.renderer.load_checkpoint(path, self._STATE.size))
+        cam = self.renderer.get_camera()
+        if cam is not None:
+            self.camera = cam
+        self.spheres = self.renderer.get_scene()
+        self.renderer.spheres = self.spheres
         st = self.sched.state
         for k in range(31):
             st.rng.state[k] = v[k]

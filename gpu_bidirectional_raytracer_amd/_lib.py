@@ -20,6 +20,7 @@ COUNTER_CAP = 30000
 BDPT_OK, BDPT_EINVAL, BDPT_EIO, BDPT_EHIP, BDPT_ENOMEM, BDPT_ESTATE = 0, -1, -2, -3, -4, -5
 DIFF, SPEC, REFR, LITE = 0, 1, 2, 3
 KEY_UP, KEY_DOWN, KEY_LEFT, KEY_RIGHT, KEY_PAGE_UP, KEY_PAGE_DOWN = range(0x101, 0x107)
+FEATURES = {1: "specialized", 2: "det_skip", 4: "zero_exit", 8: "last_skip", 16: "bvh", 32: "pass_streams"}
 
 
 class Vec(ctypes.Structure):
@@ -81,6 +82,8 @@ _SIGS = [
     ("bdpt_kernel_timing", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong), ctypes.c_int]),
     ("bdpt_scene_has_bvh", ctypes.c_int, [_P]),
     ("bdpt_last_traversal", ctypes.c_int, [_P]),
+    ("bdpt_last_kernel_features", ctypes.c_int, [_P]),
+    ("bdpt_zero_exit_safe", ctypes.c_int, [ctypes.POINTER(Sphere), ctypes.c_uint]),
     ("bdpt_light_pass", ctypes.c_int, [_P, ctypes.c_int]),
     ("bdpt_generate_rand", ctypes.c_int, [_P, ctypes.c_uint]),
     ("bdpt_path_passes", ctypes.c_int, [_P, _P, _P, ctypes.c_int]),
@@ -92,6 +95,11 @@ _SIGS = [
     ("bdpt_read_pixels", ctypes.c_int, [_P, _P]),
     ("bdpt_read_rand", ctypes.c_int, [_P, _P]),
     ("bdpt_read_lightpaths", ctypes.c_int, [_P, _P]),
+    ("bdpt_write_lightpaths", ctypes.c_int, [_P, _P]),
+    ("bdpt_rand_seed", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint)]),
+    ("bdpt_get_camera", ctypes.c_int, [_P, ctypes.POINTER(Camera)]),
+    ("bdpt_frame_size", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
+    ("bdpt_get_scene", ctypes.c_int, [_P, ctypes.POINTER(Sphere), ctypes.c_uint]),
     ("bdpt_device_buffers", ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.POINTER(_P), ctypes.POINTER(_P)]),
     ("bdpt_update_pixels", ctypes.c_int, [_P]),
     ("bdpt_write_radiance", ctypes.c_int, [_P, _P, _P]),

@@ -433,6 +433,9 @@ void bdpt_cpu_read_rand(const bdpt_cpu_ctx* c, float* t) { memcpy(t, c->rnd.data
 void bdpt_cpu_read_lightpaths(const bdpt_cpu_ctx* c, bdpt_lightpath* lp) {
     memcpy(lp, c->lp.data(), sizeof(bdpt_lightpath) * BDPT_LIGHT_POINTS);
 }
+void bdpt_cpu_write_lightpaths(bdpt_cpu_ctx* c, const bdpt_lightpath* lp) {
+    memcpy(c->lp.data(), lp, sizeof(bdpt_lightpath) * BDPT_LIGHT_POINTS);
+}
 void bdpt_cpu_update_pixels(bdpt_cpu_ctx* c) {
     for (size_t i = 0; i < c->colors.size(); i++) {
         c->pixels[4 * i] = (unsigned char)to_int8(c->colors[i].x, c->thr);

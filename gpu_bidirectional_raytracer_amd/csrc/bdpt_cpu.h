@@ -25,6 +25,7 @@ void bdpt_cpu_read_radiance(const bdpt_cpu_ctx* c, bdpt_vec* colors, unsigned* c
 void bdpt_cpu_read_pixels(const bdpt_cpu_ctx* c, unsigned char* rgba);
 void bdpt_cpu_read_rand(const bdpt_cpu_ctx* c, float* t);
 void bdpt_cpu_read_lightpaths(const bdpt_cpu_ctx* c, bdpt_lightpath* lp);
+void bdpt_cpu_write_lightpaths(bdpt_cpu_ctx* c, const bdpt_lightpath* lp);
 void bdpt_cpu_update_pixels(bdpt_cpu_ctx* c);
 void bdpt_cpu_write_radiance(bdpt_cpu_ctx* c, const bdpt_vec* colors, const unsigned* counter);
 

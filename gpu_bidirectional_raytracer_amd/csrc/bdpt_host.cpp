@@ -136,6 +136,9 @@ struct bdpt_ctx {
     std::vector<hipModule_t> jit_mods;
     char jit_err[256] = {0};            // why the last specialisation fell back (diagnostics)
     int jit_waves = 0;                  // waves/SIMD bound of the last specialised build
+    bool jit_zero_exit = false;         // the last specialised build has the black-surface exit
+    int last_features = 0;              // BDPT_FEAT_* of the last path-pass launch
+    unsigned rand_seed = 0;             // seed of the current MT607 table (rand_ready)
     char err[512] = {0};
     // multi-device context (bdpt_create_multi): this context renders on devices[0] and owns the
     // peer contexts of the other devices; the frame is assembled on devices[0] by a sum-reduce
@@ -515,43 +518,9 @@ static hipFunction_t jit_path_kernel(bdpt_ctx* c, bool streams) {
     }
     if (nl == 0) lrec += "{0,0,0,0},{0,0,0,0}";
     lrec += "}";
-    // Black-surface exit (bdpt_kernels.hip BDPT_ZERO_EXIT) is exact when the throughput before
-    // the black hit is finite (0 * thr = 0) and every later term a path could add is finite
-    // (0 * term = +0).  Scene values finite and colours <= 1e3: thr <= (4e3)^7 after 7 segments.
-    // Emission and VLP radiance <= e * 4 pi r^2 < 1e37.  The NEE term e * 4 pi r^2 * wi * wo / len^2
-    // needs len away from 0: every emitter keeps a gap >= max(1, 1e-4 * scene scale) from every
-    // other sphere's surface, far above the rounding of hit points (~2^-23 * scale).  Compiled in
-    // only when the scene has a black non-emitter (else it would only cost a test).
-    bool zero_exit = false, sane = true;
-    double scale = 0.0;
-    for (unsigned i = 0; i < n; i++) {
-        const bdpt_sphere& o = c->spheres[i];
-        const double v[10] = {o.rad, o.p.x, o.p.y, o.p.z, o.e.x, o.e.y, o.e.z, o.c.x, o.c.y, o.c.z};
-        for (double x : v) sane = sane && std::isfinite(x);
-        sane = sane && o.c.x <= 1e3f && o.c.y <= 1e3f && o.c.z <= 1e3f;
-        const double sc = sqrt((double)o.p.x * o.p.x + (double)o.p.y * o.p.y + (double)o.p.z * o.p.z) + fabs(o.rad);
-        if (sc > scale) scale = sc;
-        const bool emits = !(o.e.x == 0.f && o.e.y == 0.f && o.e.z == 0.f);
-        if (!emits && o.c.x == 0.f && o.c.y == 0.f && o.c.z == 0.f) zero_exit = true;
-    }
-    zero_exit = zero_exit && sane;
-    const double min_gap = 1e-4 * scale > 1.0 ? 1e-4 * scale : 1.0;
-    for (unsigned i = 0; i < n && zero_exit; i++) {
-        const bdpt_sphere& e = c->spheres[i];
-        if (e.e.x == 0.f && e.e.y == 0.f && e.e.z == 0.f) continue;
-        const double emax = fmax(fabs(e.e.x), fmax(fabs(e.e.y), fabs(e.e.z)));
-        if (!(emax * 4.0 * 3.14159265358979 * (double)e.rad * e.rad < 1e37)) zero_exit = false;
-        for (unsigned k = 0; k < n && zero_exit; k++) {
-            if (k == i) continue;
-            const bdpt_sphere& o = c->spheres[k];
-            const double dx = (double)e.p.x - o.p.x, dy = (double)e.p.y - o.p.y, dz = (double)e.p.z - o.p.z;
-            const double d = sqrt(dx * dx + dy * dy + dz * dz);
-            double gap = d - e.rad - o.rad;                              // apart
-            if (o.rad - d - e.rad > gap) gap = o.rad - d - e.rad;        // emitter inside o
-            if (e.rad - d - o.rad > gap) gap = e.rad - d - o.rad;        // o inside the emitter
-            if (!(gap >= min_gap)) zero_exit = false;
-        }
-    }
+    // Black-surface exit (bdpt_kernels.hip BDPT_ZERO_EXIT): compiled in only when ending a path at
+    // a black non-emitter is provably exact for this scene (bdpt_util.c bdpt_zero_exit_safe).
+    const bool zero_exit = bdpt_zero_exit_safe(c->spheres.data(), n) != 0;
     const char* wenv = getenv("BDPT_JIT_WAVES");
     int waves = wenv ? atoi(wenv) : 6;
     const std::string name = "&bdpt_path_kernel_t<" + std::to_string(n) + (streams ? ", true>" : ", false>");
@@ -606,6 +575,7 @@ static hipFunction_t jit_path_kernel(bdpt_ctx* c, bool streams) {
         if (scratch == 0 || waves <= 5 || getenv("BDPT_JIT_SCRATCH_OK")) {
             c->jit_err[0] = 0;
             c->jit_waves = waves;
+            c->jit_zero_exit = zero_exit;
             return fn;
         }
     }
@@ -852,6 +822,7 @@ static int one_generate_rand(bdpt_ctx* c, unsigned seed) {
     if (c->cpu) {
         bdpt_cpu_generate_rand(c->cpu, seed);
         c->rand_ready = true;
+        c->rand_seed = seed;
         return BDPT_OK;
     }
     HIPCHK(c, hipSetDevice(c->device));
@@ -867,6 +838,7 @@ static int one_generate_rand(bdpt_ctx* c, unsigned seed) {
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->rand_ready = true;
+    c->rand_seed = seed;
     return BDPT_OK;
 }
 
@@ -875,6 +847,7 @@ static int one_light_pass(bdpt_ctx* c, int current_sample) {
     if (c->cpu) {
         bdpt_cpu_light_pass(c->cpu, current_sample);
         c->rand_ready = true;
+        c->rand_seed = (unsigned)(current_sample * 5);
         return BDPT_OK;
     }
     // The reference regenerates the table per light with the same seed (smallpt_cpu.c:321-322):
@@ -915,6 +888,7 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
         c->last_streams = 1;
         c->last_specialized = false;
         c->last_bvh = false;
+        c->last_features = 0;
         return BDPT_OK;
     }
     HIPCHK(c, hipSetDevice(c->device));
@@ -1118,6 +1092,8 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
         const void* kern = bdpt_path_kernel_table[(a.streams > 1) * 18 + kidx];
         const hipFunction_t jf = a.streams > 1 ? jf_streams : jf_fused;
         c->last_specialized = jf != nullptr;
+        c->last_features = BDPT_FEAT_LAST_SKIP | (bvh ? BDPT_FEAT_BVH : 0) | (a.streams > 1 ? BDPT_FEAT_STREAMS : 0) |
+                           (jf ? BDPT_FEAT_SPECIALIZED | BDPT_FEAT_DET_SKIP | (c->jit_zero_exit ? BDPT_FEAT_ZERO_EXIT : 0) : 0);
         void* kargs[] = {&a};
         grid.z = a.streams;
         const int half = c->rb_next;
@@ -1248,6 +1224,50 @@ int bdpt_read_lightpaths(bdpt_ctx* c, bdpt_lightpath* lp) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return BDPT_OK;
 }
+
+static int one_write_lightpaths(bdpt_ctx* c, const bdpt_lightpath* lp) {
+    if (!c || !lp) return BDPT_EINVAL;
+    if (c->cpu) {
+        bdpt_cpu_write_lightpaths(c->cpu, lp);
+        return BDPT_OK;
+    }
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));             // queued passes may still read dev_lp
+    HIPCHK(c, hipMemcpyAsync(c->d_lp, lp, sizeof(bdpt_lightpath) * BDPT_LIGHT_POINTS, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return BDPT_OK;
+}
+
+int bdpt_rand_seed(const bdpt_ctx* c, unsigned* seed) {
+    if (!c || !seed) return BDPT_EINVAL;
+    if (!c->rand_ready) return BDPT_ESTATE;
+    *seed = c->rand_seed;
+    return BDPT_OK;
+}
+
+int bdpt_get_camera(const bdpt_ctx* c, bdpt_camera* cam) {
+    if (!c || !cam) return BDPT_EINVAL;
+    if (!c->cam_set) return BDPT_ESTATE;
+    *cam = c->cam;
+    return BDPT_OK;
+}
+
+int bdpt_get_scene(const bdpt_ctx* c, bdpt_sphere* spheres, unsigned cap) {
+    if (!c) return BDPT_EINVAL;
+    const unsigned n = (unsigned)c->spheres.size();
+    if (spheres)
+        for (unsigned i = 0; i < n && i < cap; i++) spheres[i] = c->spheres[i];
+    return (int)n;
+}
+
+int bdpt_frame_size(const bdpt_ctx* c, int* W, int* H) {
+    if (!c || !W || !H) return BDPT_EINVAL;
+    *W = c->W;
+    *H = c->H;
+    return BDPT_OK;
+}
+
+int bdpt_last_kernel_features(const bdpt_ctx* c) { return c ? c->last_features : BDPT_EINVAL; }
 
 static int one_device_buffers(bdpt_ctx* c, void** colors, void** counter, void** pixels) {
     if (!c) return BDPT_EINVAL;
@@ -1553,6 +1573,10 @@ int bdpt_kernel_timing(bdpt_ctx* c, double* kernel_ms, long long* launches, int 
     return BDPT_OK;
 }
 // Read-back of a multi-device context reads the assembled frame.
+int bdpt_write_lightpaths(bdpt_ctx* c, const bdpt_lightpath* lp) {
+    if (int rc = one_write_lightpaths(c, lp)) return rc;
+    return forward(c, [&](bdpt_ctx* p) { return one_write_lightpaths(p, lp); });
+}
 int bdpt_read_radiance(bdpt_ctx* c, bdpt_vec* colors, unsigned* counter) {
     if (!c) return BDPT_EINVAL;
     if (!c->multi) return one_read_radiance(c, colors, counter);
@@ -1627,61 +1651,8 @@ int bdpt_write_radiance(bdpt_ctx* c, const bdpt_vec* colors, const unsigned* cou
     return forward(c, [&](bdpt_ctx* p) { return one_write_radiance(p, colors, counter, true); });
 }
 
-namespace {
-const char kCkptMagic[8] = {'B', 'D', 'P', 'T', 'C', 'K', 'P', '1'};
-struct ckpt_header {
-    char magic[8];
-    int width, height;
-    unsigned host_bytes, reserved;
-};
-}  // namespace
-
-int bdpt_save_checkpoint(bdpt_ctx* c, const char* path, const void* host_state, unsigned host_bytes) {
-    if (!c || !path || (host_bytes && !host_state)) return BDPT_EINVAL;
-    const size_t np = (size_t)c->W * c->H;
-    std::vector<bdpt_vec> col(np);
-    std::vector<unsigned> cnt(np);
-    if (int rc = bdpt_read_radiance(c, col.data(), cnt.data())) return rc;
-    ckpt_header h;
-    memcpy(h.magic, kCkptMagic, 8);
-    h.width = c->W; h.height = c->H; h.host_bytes = host_bytes; h.reserved = 0;
-    const std::string tmp = std::string(path) + ".tmp." + std::to_string((long)getpid());
-    FILE* f = fopen(tmp.c_str(), "wb");
-    if (!f) return fail(c, BDPT_EIO, "bdpt_save_checkpoint: cannot open %s", tmp.c_str());
-    bool ok = fwrite(&h, sizeof h, 1, f) == 1 && fwrite(col.data(), sizeof(bdpt_vec), np, f) == np &&
-              fwrite(cnt.data(), sizeof(unsigned), np, f) == np &&
-              (host_bytes == 0 || fwrite(host_state, 1, host_bytes, f) == host_bytes);
-    ok = (fflush(f) == 0) && ok;
-    ok = (fclose(f) == 0) && ok;
-    if (ok) ok = rename(tmp.c_str(), path) == 0;
-    if (!ok) {
-        unlink(tmp.c_str());
-        return fail(c, BDPT_EIO, "bdpt_save_checkpoint: cannot write %s", path);
-    }
-    return BDPT_OK;
-}
-
-int bdpt_load_checkpoint(bdpt_ctx* c, const char* path, void* host_state, unsigned host_bytes) {
-    if (!c || !path || (host_bytes && !host_state)) return BDPT_EINVAL;
-    FILE* f = fopen(path, "rb");
-    if (!f) return fail(c, BDPT_EIO, "bdpt_load_checkpoint: cannot open %s", path);
-    ckpt_header h;
-    const size_t np = (size_t)c->W * c->H;
-    std::vector<bdpt_vec> col(np);
-    std::vector<unsigned> cnt(np);
-    int rc = BDPT_OK;
-    if (fread(&h, sizeof h, 1, f) != 1 || memcmp(h.magic, kCkptMagic, 8) != 0)
-        rc = fail(c, BDPT_EIO, "bdpt_load_checkpoint: %s is not a checkpoint", path);
-    else if (h.width != c->W || h.height != c->H || h.host_bytes != host_bytes)
-        rc = fail(c, BDPT_EINVAL, "bdpt_load_checkpoint: %s holds %dx%d with %u host bytes, not %dx%d with %u",
-                  path, h.width, h.height, h.host_bytes, c->W, c->H, host_bytes);
-    else if (fread(col.data(), sizeof(bdpt_vec), np, f) != np || fread(cnt.data(), sizeof(unsigned), np, f) != np ||
-             (host_bytes && fread(host_state, 1, host_bytes, f) != host_bytes))
-        rc = fail(c, BDPT_EIO, "bdpt_load_checkpoint: %s is truncated", path);
-    fclose(f);
-    if (rc) return rc;
-    return bdpt_write_radiance(c, col.data(), cnt.data());
-}
+// bdpt_save_checkpoint / bdpt_load_checkpoint: bdpt_ckpt.c (over the entry points above)
+int bdpt__fail(bdpt_ctx* c, int code, const char* msg) { return fail(c, code, "%s", msg); }
 
 }  // extern "C"
 

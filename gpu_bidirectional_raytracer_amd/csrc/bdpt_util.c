@@ -300,3 +300,63 @@ void bdpt_gamma_thresholds(float thr[256])
         memcpy(&thr[k], &lo, 4);
     }
 }
+
+/* The black-surface exit rule (bdpt_kernels.hip BDPT_ZERO_EXIT, include/bdpt.h).  A hit on a black
+ * non-emitter multiplies the reference's throughput by c = 0 (device.cu:665/711/732/758-765), and
+ * the path then runs on to its 7th segment (:621), adding thr * term at every later vertex
+ * (:656, :671-672).  With thr == +-0 every such addition is +-0 -- and rad + (+-0) == rad -- exactly
+ * when every term is finite.  This proves it for the scene, in double arithmetic with margins:
+ *  - all scene values finite, every |c| <= 1e3 (then the throughput before the black hit is at
+ *    most (4 * 1e3)^7: the refraction weights Re/P and Tr/(1-P) are <= 4, :754-755), and every
+ *    sphere radius > 2^-16 * scene scale (a hit point then lies far above rounding from its
+ *    sphere's centre, so the normal of :640-641 is not 0/0);
+ *  - emission: thr * e * |dp| (:654-656), |dp| <= 1 + eps;
+ *  - NEE (:470-505): per emitter e * 4 pi r^2 * wi * wo / len^2 with wi, wo <= 1 + eps; a path
+ *    vertex never lies on an emitter (a hit on one ends the path, :652-661) and every emitter keeps
+ *    a gap >= max(1, 1e-4 * scale) from every other sphere's surface, so len >= ~1;
+ *  - VLP (:510-537): rad * wi * wo, no 1/len^2; a VLP carries e/2 (escaped light ray) or
+ *    VecMultiply(e/4, c) (:268, :279-337), so |rad| <= 0.5 * |e| * max(1, |c|); wo uses the
+ *    escaped VLP's normal (-(o - p) / r), whose length is within 8 * 2^-24 * (|p| + r) / r of 1;
+ *  - the vertex's sum NEE + VLP (:539-540) stays below FLT_MAX: n_lights * max(e * 4 pi r^2) * 1.1
+ *    + 0.5 * max|e| * max(1, max|c|) * g < 1e38 (g: the normal-length factor above).
+ * Scenes without a black non-emitter return 0 (the exit would only cost a test). */
+int bdpt_zero_exit_safe(const bdpt_sphere *s, unsigned n)
+{
+    if (!s || n == 0) return 0;
+    double scale = 0.0, cmax = 0.0, emax = 0.0, nee = 0.0, g = 1.0;
+    int black = 0;
+    for (unsigned i = 0; i < n; i++) {
+        const bdpt_sphere *o = &s[i];
+        const double v[10] = {o->rad, o->p.x, o->p.y, o->p.z, o->e.x, o->e.y, o->e.z, o->c.x, o->c.y, o->c.z};
+        for (int k = 0; k < 10; k++)
+            if (!isfinite(v[k])) return 0;
+        const double sc = sqrt(v[1] * v[1] + v[2] * v[2] + v[3] * v[3]) + fabs(v[0]);
+        if (sc > scale) scale = sc;
+        for (int k = 7; k < 10; k++) cmax = fmax(cmax, fabs(v[k]));
+        const int emits = !(o->e.x == 0.f && o->e.y == 0.f && o->e.z == 0.f);
+        if (!emits && o->c.x == 0.f && o->c.y == 0.f && o->c.z == 0.f) black = 1;
+    }
+    if (!black || !(cmax <= 1e3)) return 0;
+    const double min_gap = fmax(1.0, 1e-4 * scale), min_rad = ldexp(scale, -16);
+    for (unsigned i = 0; i < n; i++) {
+        const bdpt_sphere *e = &s[i];
+        const double re = fabs((double)e->rad);
+        if (!(re > min_rad)) return 0;
+        if (e->e.x == 0.f && e->e.y == 0.f && e->e.z == 0.f) continue;
+        const double em = fmax(fabs(e->e.x), fmax(fabs(e->e.y), fabs(e->e.z)));
+        emax = fmax(emax, em);
+        nee += em * 4.0 * 3.14159265358979323846 * re * re;
+        const double pn = sqrt((double)e->p.x * e->p.x + (double)e->p.y * e->p.y + (double)e->p.z * e->p.z);
+        g = fmax(g, 1.0 + 8.0 * ldexp(pn + re, -24) / re);
+        for (unsigned k = 0; k < n; k++) {
+            if (k == i) continue;
+            const bdpt_sphere *o = &s[k];
+            const double ro = fabs((double)o->rad);
+            const double dx = (double)e->p.x - o->p.x, dy = (double)e->p.y - o->p.y, dz = (double)e->p.z - o->p.z;
+            const double d = sqrt(dx * dx + dy * dy + dz * dz);
+            const double gap = fmax(d - re - ro, fmax(ro - d - re, re - d - ro));   /* apart / inside */
+            if (!(gap >= min_gap)) return 0;
+        }
+    }
+    return nee * 1.1 + 0.5 * emax * fmax(1.0, cmax) * g < 1e38;
+}

@@ -16,8 +16,9 @@
  * --gpus N (devices 0..N-1) or --devices LIST renders one frame on several GPUs of this process
  * (bdpt_create_multi: pixel bands of --tile rows, default 8, frame assembled by an RCCL reduce);
  * --seed S seeds the pass offsets' rand() (default 1: the reference never calls srand).
- * --checkpoint F saves the accumulation and the pass schedule at the end; --resume F restores
- * them after the first light pass, so a run continues exactly where the saved one stopped.
+ * --checkpoint F saves the accumulation, the pass schedule and the render state (camera, scene,
+ * MT table seed, VLPs: keys may have edited them) at the end; --resume F restores all of it after
+ * the first light pass, so a run continues exactly where the saved one stopped.
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -242,6 +243,18 @@ int main(int argc, char **argv)
         h.reinit_counter = st.reinit_counter;
         h.current_sphere = st.current_sphere;
         h.total_time = st.total_time;
+        /* the checkpoint restored the context's camera and scene (edited by keys before the
+         * save, perhaps): take them over, so later keys continue from the saved state */
+        (void)bdpt_get_camera(h.ctx, &h.camera);
+        const int n = bdpt_get_scene(h.ctx, NULL, 0);
+        if (n > 0 && (unsigned)n != h.n) {
+            bdpt_sphere *sp = malloc(sizeof(bdpt_sphere) * (size_t)n);
+            if (!sp) { bdpt_destroy(h.ctx); return 1; }
+            if (npos == 3) bdpt_free_scene(h.spheres); else free(h.spheres);
+            h.spheres = sp;
+            npos = 0;                                          /* now malloc'd here: free() */
+        }
+        if (n >= 0) h.n = (unsigned)bdpt_get_scene(h.ctx, h.spheres, (unsigned)(n > 0 ? n : 0));
         fprintf(stderr, "Resumed at pass %d\n", h.current_sample);
     }
     for (int done = 0; done < spp; done += batch)

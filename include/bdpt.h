@@ -128,6 +128,22 @@ int  bdpt_set_traversal(bdpt_ctx *ctx, int mode);
 int  bdpt_scene_has_bvh(const bdpt_ctx *ctx);
 /* BDPT_TRAVERSE_BVH or BDPT_TRAVERSE_BRUTE: what the last bdpt_path_passes call used. */
 int  bdpt_last_traversal(const bdpt_ctx *ctx);
+/* What the kernel of the last bdpt_path_passes call compiled in (no reference counterpart; none of
+ * these changes a result): bit flags below.  The three skips leave out work whose result the
+ * reference computes and never uses, so a FLOP model priced on the reference's work counts more
+ * than the kernel executes ("reference-equivalent" FLOPs). */
+#define BDPT_FEAT_SPECIALIZED 1             /* scene-specialised build (hipRTC)              */
+#define BDPT_FEAT_DET_SKIP    2             /* whole-wave skip of sphere tests all lanes miss */
+#define BDPT_FEAT_ZERO_EXIT   4             /* paths end at a black non-emitter              */
+#define BDPT_FEAT_LAST_SKIP   8             /* no next direction after the 7th segment        */
+#define BDPT_FEAT_BVH        16             /* BVH traversal (large scenes)                   */
+#define BDPT_FEAT_STREAMS    32             /* pass streams (one pass per lane + ordered fold)*/
+int  bdpt_last_kernel_features(const bdpt_ctx *ctx);
+/* The black-surface exit rule (BDPT_FEAT_ZERO_EXIT): 1 if ending a path at a black non-emitter is
+ * provably exact for this scene -- every term the reference adds after the black hit is finite,
+ * so 0 * term = +0 leaves the radiance bit-identical -- else 0.  Pure host function: the
+ * specialised build asks it, and tests check it against the Python restatement. */
+int  bdpt_zero_exit_safe(const bdpt_sphere *spheres, unsigned n_spheres);
 
 /* UpdateRendering2 smallpt_cpu.c:300-362: for every emitter in sphere order,
  * seedMTGPU(current_sample*5) + RandomGPU (MT607 table), GetRayKernel and
@@ -157,6 +173,17 @@ int  bdpt_read_radiance(bdpt_ctx *ctx, bdpt_vec *colors, unsigned *counter);
 int  bdpt_read_pixels(bdpt_ctx *ctx, unsigned char *rgba);
 int  bdpt_read_rand(bdpt_ctx *ctx, float *rand_table);          /* d_Rand, BDPT_RAND_N */
 int  bdpt_read_lightpaths(bdpt_ctx *ctx, bdpt_lightpath *lp);   /* dev_lp, 4096        */
+/* Upload all 4096 VLPs (the counterpart of bdpt_read_lightpaths; checkpoint restore). */
+int  bdpt_write_lightpaths(bdpt_ctx *ctx, const bdpt_lightpath *lp);
+/* The seed of the current MT607 table (current_sample * 5 of the last light pass, or the
+ * bdpt_generate_rand argument); BDPT_ESTATE before any table exists. */
+int  bdpt_rand_seed(const bdpt_ctx *ctx, unsigned *seed);
+/* The context's camera (BDPT_ESTATE if none was set) and scene: bdpt_get_scene copies at most
+ * `cap` spheres and returns the scene's sphere count (spheres may be NULL to ask the count). */
+int  bdpt_get_camera(const bdpt_ctx *ctx, bdpt_camera *camera);
+/* The frame size the context was created with (internal W, H). */
+int  bdpt_frame_size(const bdpt_ctx *ctx, int *width, int *height);
+int  bdpt_get_scene(const bdpt_ctx *ctx, bdpt_sphere *spheres, unsigned cap);
 /* Device pointers for zero-copy collectives (RCCL reduce of the radiance frame).  Path passes
  * run asynchronously on the context's own stream: bdpt_synchronize() before using them.  For a
  * multi-device context: the assembled frame on devices[0]. */
@@ -169,9 +196,14 @@ int  bdpt_update_pixels(bdpt_ctx *ctx);
 /* Upload colors/counter (W*H each; the counterpart of bdpt_read_radiance); pixels are
  * recomputed.  Rendering then continues from that state bit for bit. */
 int  bdpt_write_radiance(bdpt_ctx *ctx, const bdpt_vec *colors, const unsigned *counter);
-/* File = header {"BDPTCKP1", W, H, host_bytes} + colors + counter + host_bytes of caller state
- * (e.g. its bdpt_pass_state and current_sample, so the pass schedule resumes too).  Written to a
- * temporary file and renamed into place.  Load checks W, H and host_bytes against the context. */
+/* File = header {"BDPTCKP2", W, H, host_bytes, n_spheres, table seed, flags} + camera + spheres +
+ * the 4096 VLPs + colors + counter + host_bytes of caller state (e.g. its bdpt_pass_state and
+ * current_sample, so the pass schedule resumes too).  The render state travels with the frame: a
+ * run whose camera or scene was edited (KeyFunc -> ReInit / ReInitScene) resumes with the edited
+ * camera, scene, MT table and VLPs, not the scene file's.  Written to a temporary file, flushed to
+ * disk (fsync) and renamed into place.  Load checks W, H and host_bytes against the context, then
+ * restores scene, camera, table, VLPs and accumulation (the caller re-reads its own copies with
+ * bdpt_get_camera / bdpt_get_scene). */
 int  bdpt_save_checkpoint(bdpt_ctx *ctx, const char *path, const void *host_state, unsigned host_bytes);
 int  bdpt_load_checkpoint(bdpt_ctx *ctx, const char *path, void *host_state, unsigned host_bytes);
 

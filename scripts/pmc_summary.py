@@ -33,11 +33,23 @@ if len(sys.argv) > 4:
         if lines:
             cfg = json.loads(lines[-1])["config"]
             break
-    rec = {"valu_busy": round(g('SQ_INSTS_VALU') * 2 / (4 * 256 * cyc), 4),
+    rec = {"workload": cfg.get("workload", "cornell1080").split(":")[0],
+           "valu_busy": round(g('SQ_INSTS_VALU') * 2 / (4 * 256 * cyc), 4),
            "valu_lane_utilisation": round(g('SQ_THREAD_CYCLES_VALU') / (64 * g('SQ_ACTIVE_INST_VALU')), 4),
            "l2_hit_rate": round(g('TCC_HIT_sum') / (g('TCC_HIT_sum') + g('TCC_MISS_sum')), 4),
+           "wait_frac": round(g('SQ_WAIT_ANY') / g('SQ_WAVE_CYCLES'), 4),
+           "issue_stall_frac": round(g('SQ_WAIT_INST_ANY') / g('SQ_WAVE_CYCLES'), 4),
+           "active_frac": round(g('SQ_ACTIVE_INST_ANY') / g('SQ_WAVE_CYCLES'), 4),
+           "valu_insts_per_wave": round(g('SQ_INSTS_VALU') / g('SQ_WAVES'), 1),
+           "fetch_reported_kib": g('FETCH_SIZE'), "write_reported_kib": g('WRITE_SIZE'),
            "scene": cfg.get("scene"), "width": cfg.get("width"), "height": cfg.get("height"),
            "passes_per_launch": cfg.get("passes_per_step"), "pass_streams": cfg.get("pass_streams"), "specialized": cfg.get("specialized", False),
            "source": "rocprofv3 --pmc SQ_INSTS_VALU / SQ_THREAD_CYCLES_VALU / SQ_ACTIVE_INST_VALU / "
                      "GRBM_GUI_ACTIVE / TCC_HIT_sum / TCC_MISS_sum (separate passes), scripts/pmc_summary.py"}
-    json.dump(rec, open(sys.argv[4], "w"), indent=1)
+    rec = {k: (None if isinstance(v, float) and v != v else v) for k, v in rec.items()}   # NaN -> null
+    out = sys.argv[4]
+    data = json.load(open(out)) if os.path.exists(out) else {}
+    if "scene" in data:                                   # an older single-record file
+        data = {data.get("workload", "cornell1080"): data}
+    data[rec["workload"]] = rec
+    json.dump(data, open(out, "w"), indent=1)

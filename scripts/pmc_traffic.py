@@ -65,6 +65,11 @@ rec = {"workload": cfg.get("workload", "cornell1080").split(":")[0], "scene": cf
        "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), x1024, calibrated",
        "method": __doc__}
 os.makedirs(os.path.dirname(out), exist_ok=True)
-json.dump(rec, open(out, "w"), indent=1)
+# one record per workload: {workload: record}
+data = json.load(open(out)) if os.path.exists(out) else {}
+if "scene" in data:                                       # an older single-record file
+    data = {data.get("workload", "cornell1080"): data}
+data[rec["workload"]] = rec
+json.dump(data, open(out, "w"), indent=1)
 print(json.dumps({k: v for k, v in rec.items() if k not in ("method", "calibration")}))
 print(json.dumps(calib))

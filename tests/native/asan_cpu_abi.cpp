@@ -16,6 +16,9 @@ struct bdpt_ctx {
     bdpt_cpu_ctx* cpu = nullptr;
     int W = 0, H = 0;
     bool rand_ready = false, cam_set = false;
+    unsigned seed = 0;
+    bdpt_camera cam{};
+    std::vector<bdpt_sphere> spheres;
     char err[256] = {0};
 };
 
@@ -44,6 +47,7 @@ int bdpt_create(bdpt_ctx** out, const bdpt_sphere* s, unsigned n, int W, int H, 
     if (got != 1) return fail(nullptr, BDPT_EIO, "initMTGPU(): failed to load %s", dat);
     bdpt_ctx* c = new bdpt_ctx();
     c->cpu = bdpt_cpu_create(s, n, W, H, params);
+    c->spheres.assign(s, s + n);
     c->W = W;
     c->H = H;
     *out = c;
@@ -61,12 +65,44 @@ void bdpt_destroy(bdpt_ctx* c) {
 }
 int bdpt_num_devices(const bdpt_ctx*) { return 1; }
 const char* bdpt_reduce_backend(const bdpt_ctx*) { return "none"; }
-int bdpt_set_scene(bdpt_ctx* c, const bdpt_sphere* s, unsigned n) { bdpt_cpu_set_scene(c->cpu, s, n); return BDPT_OK; }
+int bdpt_set_scene(bdpt_ctx* c, const bdpt_sphere* s, unsigned n) {
+    bdpt_cpu_set_scene(c->cpu, s, n);
+    c->spheres.assign(s, s + n);
+    return BDPT_OK;
+}
 int bdpt_set_camera(bdpt_ctx* c, const bdpt_camera* cam) {
     bdpt_cpu_set_camera(c->cpu, cam);
+    c->cam = *cam;
     c->cam_set = true;
     return BDPT_OK;
 }
+int bdpt_get_camera(const bdpt_ctx* c, bdpt_camera* cam) {
+    if (!c->cam_set) return BDPT_ESTATE;
+    *cam = c->cam;
+    return BDPT_OK;
+}
+int bdpt_get_scene(const bdpt_ctx* c, bdpt_sphere* s, unsigned cap) {
+    for (unsigned i = 0; s && i < c->spheres.size() && i < cap; i++) s[i] = c->spheres[i];
+    return (int)c->spheres.size();
+}
+int bdpt_frame_size(const bdpt_ctx* c, int* W, int* H) {
+    *W = c->W;
+    *H = c->H;
+    return BDPT_OK;
+}
+int bdpt_generate_rand(bdpt_ctx* c, unsigned seed) {
+    bdpt_cpu_generate_rand(c->cpu, seed);
+    c->rand_ready = true;
+    c->seed = seed;
+    return BDPT_OK;
+}
+int bdpt_rand_seed(const bdpt_ctx* c, unsigned* seed) {
+    if (!c->rand_ready) return BDPT_ESTATE;
+    *seed = c->seed;
+    return BDPT_OK;
+}
+int bdpt_read_lightpaths(bdpt_ctx* c, bdpt_lightpath* lp) { bdpt_cpu_read_lightpaths(c->cpu, lp); return BDPT_OK; }
+int bdpt_write_lightpaths(bdpt_ctx* c, const bdpt_lightpath* lp) { bdpt_cpu_write_lightpaths(c->cpu, lp); return BDPT_OK; }
 int bdpt_reset_accum(bdpt_ctx* c) { bdpt_cpu_reset_accum(c->cpu); return BDPT_OK; }
 int bdpt_set_shard(bdpt_ctx* c, int shard, int nshards, int band) {
     if (nshards < 1 || shard < 0 || shard >= nshards || band < 1) return fail(c, BDPT_EINVAL, "bad shard");
@@ -76,6 +112,7 @@ int bdpt_set_shard(bdpt_ctx* c, int shard, int nshards, int band) {
 int bdpt_light_pass(bdpt_ctx* c, int current_sample) {
     bdpt_cpu_light_pass(c->cpu, current_sample);
     c->rand_ready = true;
+    c->seed = (unsigned)(current_sample * 5);
     return BDPT_OK;
 }
 int bdpt_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int npass) {
@@ -91,37 +128,7 @@ int bdpt_write_radiance(bdpt_ctx* c, const bdpt_vec* col, const unsigned* cnt) {
     return BDPT_OK;
 }
 
-// The checkpoint file format of bdpt_host.cpp, restated for the sanitizer build.
-int bdpt_save_checkpoint(bdpt_ctx* c, const char* path, const void* st, unsigned bytes) {
-    const size_t np = (size_t)c->W * c->H;
-    std::vector<bdpt_vec> col(np);
-    std::vector<unsigned> cnt(np);
-    bdpt_cpu_read_radiance(c->cpu, col.data(), cnt.data());
-    FILE* f = fopen(path, "wb");
-    if (!f) return fail(c, BDPT_EIO, "cannot write %s", path);
-    const int hdr[4] = {c->W, c->H, (int)bytes, 0};
-    bool ok = fwrite("BDPTCKP1", 1, 8, f) == 8 && fwrite(hdr, sizeof hdr, 1, f) == 1 &&
-              fwrite(col.data(), sizeof(bdpt_vec), np, f) == np && fwrite(cnt.data(), 4, np, f) == np &&
-              (!bytes || fwrite(st, 1, bytes, f) == bytes);
-    ok = fclose(f) == 0 && ok;
-    return ok ? BDPT_OK : fail(c, BDPT_EIO, "cannot write %s", path);
-}
-int bdpt_load_checkpoint(bdpt_ctx* c, const char* path, void* st, unsigned bytes) {
-    const size_t np = (size_t)c->W * c->H;
-    std::vector<bdpt_vec> col(np);
-    std::vector<unsigned> cnt(np);
-    FILE* f = fopen(path, "rb");
-    if (!f) return fail(c, BDPT_EIO, "cannot open %s", path);
-    char magic[8];
-    int hdr[4];
-    bool ok = fread(magic, 1, 8, f) == 8 && !memcmp(magic, "BDPTCKP1", 8) && fread(hdr, sizeof hdr, 1, f) == 1 &&
-              hdr[0] == c->W && hdr[1] == c->H && hdr[2] == (int)bytes &&
-              fread(col.data(), sizeof(bdpt_vec), np, f) == np && fread(cnt.data(), 4, np, f) == np &&
-              (!bytes || fread(st, 1, bytes, f) == bytes);
-    fclose(f);
-    if (!ok) return fail(c, BDPT_EIO, "bad checkpoint %s", path);
-    bdpt_cpu_write_radiance(c->cpu, col.data(), cnt.data());
-    return BDPT_OK;
-}
+// checkpoint / resume: the product's own bdpt_ckpt.c, linked in, over the entry points above
+int bdpt__fail(bdpt_ctx* c, int code, const char* msg) { return fail(c, code, "%s", msg); }
 
 }  // extern "C"

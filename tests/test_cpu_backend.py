@@ -164,3 +164,72 @@ def test_smallpt_host_on_cpu_matches_oracle_replay(tmp_path):
         for _ in range(3):
             ora.IdleFunc()
     assert np.array_equal(_read_ppm(out), ora.pixels[..., :3].astype(np.int64))
+
+
+def test_mirror_resume_after_camera_and_scene_keys(tmp_path):
+    """A checkpoint taken after KeyFunc edits (a camera move -> ReInit, a sphere selection and move
+    -> ReInitScene) carries the edited camera, scene, MT table and VLPs: a fresh SmallPT that loads
+    it and continues (more passes, another camera key) equals the uninterrupted session bit for
+    bit, and its own camera/spheres are the edited ones."""
+    scn = os.path.join(SCENES, "cornell.scn")
+
+    def session(ck=None, upto=False):
+        s = g.SmallPT(30, 22, scn, device=CPU)
+        s.IdleFunc()
+        s.UpdateRendering(2)
+        for k in "w+4":
+            s.KeyFunc(k)
+            s.UpdateRendering(2)
+        if ck:
+            s.SaveCheckpoint(ck)
+        return s
+
+    def tail(s):
+        s.UpdateRendering(3)
+        s.KeyFunc("d")
+        s.UpdateRendering(2)
+        col, cnt = s.colors()
+        return col, cnt, s.pixels()
+
+    ref_s = session()
+    edited_cam = bytes(ref_s.camera)
+    edited_sp = ref_s.spheres.copy()
+    ref = tail(ref_s)
+    ref_s.FreeBuffers()
+    ck = str(tmp_path / "k.ckpt")
+    session(ck).FreeBuffers()
+    s = g.SmallPT(30, 22, scn, device=CPU)                  # starts from the scene file
+    s.IdleFunc()
+    s.LoadCheckpoint(ck)
+    assert bytes(s.camera) == edited_cam and np.array_equal(s.spheres, edited_sp)
+    out = tail(s)
+    for a, b, w in zip(out, ref, ("colors", "counter", "pixels")):
+        same(a, b, f"resumed after keys: {w}")
+    s.FreeBuffers()
+
+
+def test_smallpt_host_resume_after_keys_matches_oracle_replay(tmp_path):
+    """The C host (--device -1) saves after camera / sphere keys and resumes in a fresh process:
+    the resumed run continues with the edited camera and scene, and its final frame equals the
+    oracle's host-loop restatement of the whole session."""
+    from oracle.replay import Session
+    env = dict(os.environ, BDPT_CPU_THREADS="4")
+    dat = os.path.join(REPO, "assets", "data", "MersenneTwister.dat")
+    base = [SMALLPT, "24", "18", os.path.join(SCENES, "cornell.scn"), "--spp", "3", "--batch", "2",
+            "--device", "-1", "--dat", dat]
+    ck, out = tmp_path / "s.ckpt", tmp_path / "s.ppm"
+    subprocess.check_call(base + ["--keys", "w+4", "--checkpoint", str(ck)], cwd=tmp_path, env=env,
+                          timeout=300, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    r = subprocess.run(base + ["--keys", "d", "--resume", str(ck), "--out", str(out)], cwd=tmp_path,
+                       env=env, timeout=300, capture_output=True, text=True)
+    assert r.returncode == 0 and "Resumed at pass" in r.stderr, r.stderr
+    cam, sp = g.read_scene(os.path.join(SCENES, "cornell.scn"))
+    o = np.array([cam.orig.x, cam.orig.y, cam.orig.z], np.float32)
+    t = np.array([cam.target.x, cam.target.y, cam.target.z], np.float32)
+    ora = Session(sp, o, t, 25, 19)
+    for k in (None, "w", "+", "4", None, "d"):            # None: the resumed run's first passes
+        if k is not None:
+            ora.KeyFunc(k)
+        for _ in range(3):
+            ora.IdleFunc()
+    assert np.array_equal(_read_ppm(out), ora.pixels[..., :3].astype(np.int64))

@@ -109,3 +109,46 @@ def test_smallpt_host_resume(gpu, tmp_path):
                        timeout=120, capture_output=True, text=True)
     assert r.returncode == 0 and "Resumed at pass 5" in r.stderr, r.stderr
     assert filecmp.cmp(full, part, shallow=False)
+
+
+@pytest.mark.parametrize("devices", [None, [0, 0]])
+def test_mirror_resume_after_keys(gpu, tmp_path, devices):
+    """A checkpoint taken after camera / sphere keys restores the edited camera, scene, MT table
+    and VLPs (bdpt_ckpt.c): the resumed session equals the uninterrupted one bit for bit (one
+    device, and a two-shard multi-device context)."""
+    scn = os.path.join(SCENES, "cornell_glass.scn")
+
+    def start():
+        s = g.SmallPT(40, 30, scn, device=gpu)
+        if devices is not None:                          # swap in a multi-device context
+            s.renderer.close()
+            s.renderer = g.Renderer(s.spheres, s.width, s.height, s.camera, s.dat_path, devices=devices)
+        return s
+
+    def head(s):
+        s.IdleFunc()
+        s.UpdateRendering(2)
+        for k in "s+8":
+            s.KeyFunc(k)
+            s.UpdateRendering(3)
+
+    def tail(s):
+        s.UpdateRendering(4)
+        s.KeyFunc("a")
+        s.UpdateRendering(2)
+        return frame(s.renderer)
+
+    a = start()
+    head(a)
+    ref = tail(a)
+    a.FreeBuffers()
+    b = start()
+    head(b)
+    ck = str(tmp_path / "keys.ckpt")
+    b.SaveCheckpoint(ck)
+    b.FreeBuffers()
+    c = start()
+    c.IdleFunc()
+    c.LoadCheckpoint(ck)
+    same(tail(c), ref, "resume after keys")
+    c.FreeBuffers()

@@ -8,6 +8,7 @@ import os
 import subprocess
 import sys
 
+import numpy as np
 import pytest
 
 from conftest import REPO, SCENES
@@ -61,10 +62,21 @@ def test_specialised_build_offline(scene):
     assert r.returncode == 0, r.stdout + r.stderr
 
 
+def _c_rule(sp):
+    import ctypes
+    sys.path.insert(0, REPO)
+    import gpu_bidirectional_raytracer_amd as g
+    arr = g.spheres_to_array(sp)
+    return bool(g._lib.lib.bdpt_zero_exit_safe(ctypes.cast(ctypes.c_void_p(arr.ctypes.data),
+                                                           ctypes.POINTER(g.Sphere)), len(arr)))
+
+
 def test_zero_exit_rule():
     """The black-surface path exit (bdpt_kernels.hip BDPT_ZERO_EXIT) is compiled in only for scenes
-    with a black non-emitter whose emitters keep a gap >= 1 from every other surface (the rule of
-    bdpt_host.cpp jit_path_kernel, mirrored by tools/jit_codegen_check.py)."""
+    with a black non-emitter whose emitters keep a gap >= 1 from every other surface and whose
+    post-black terms are provably finite.  The decision the host makes (bdpt_util.c
+    bdpt_zero_exit_safe, called by jit_path_kernel) and its Python restatement
+    (tools/jit_codegen_check.py) must agree."""
     import jit_codegen_check as jc
     sys.path.insert(0, REPO)
     import gpu_bidirectional_raytracer_amd as g
@@ -73,7 +85,61 @@ def test_zero_exit_rule():
     for scene, safe in want.items():
         _, sp = g.read_scene(os.path.join(SCENES, scene + ".scn"))
         assert jc.zero_exit_safe(sp) == safe, scene
-    # a light touching a black wall: no exit
-    _, sp = g.read_scene(os.path.join(SCENES, "cornell.scn"))
-    sp[8]["p"] = [50.0, 81.6 - 7.5, 81.6]
-    assert not jc.zero_exit_safe(sp)
+        assert _c_rule(sp) == safe, scene
+    _, base = g.read_scene(os.path.join(SCENES, "cornell.scn"))
+    light = int(next(i for i, s in enumerate(base) if any(float(v) != 0 for v in s["e"])))
+
+    def variant(edit):
+        sp = base.copy()
+        for (idx, field), val in edit.items():
+            sp[idx][field] = val
+        return sp
+
+    cases = [
+        # a light touching a black wall: no exit
+        ({(light, "p"): [50.0, 81.6 - 7.5, 81.6]}, False),
+        # a small, very hot emitter: e * 4 pi r^2 below 1e37, but its VLPs carry 0.25 e c -> inf
+        ({(light, "rad"): 0.5, (light, "e"): [3e36, 3e36, 3e36], (0, "c"): [1e3, 1e3, 1e3]}, False),
+        # the same emitter with unit colours: finite
+        ({(light, "rad"): 0.5, (light, "e"): [3e36, 3e36, 3e36]}, True),
+        # a negative colour beyond 1e3: the throughput before the black hit could overflow
+        ({(0, "c"): [-1e30, 0.5, 0.5]}, False),
+        ({(0, "c"): [-0.5, 0.5, 0.5]}, True),
+        # non-finite values
+        ({(0, "c"): [float("nan"), 0.5, 0.5]}, False),
+        ({(light, "e"): [float("inf"), 1.0, 1.0]}, False),
+        # a degenerate sphere (radius 0)
+        ({(1, "rad"): 0.0}, False),
+    ]
+    for edit, safe in cases:
+        sp = variant(edit)
+        assert jc.zero_exit_safe(sp) == safe, edit
+        assert _c_rule(sp) == safe, edit
+    # many emitters whose NEE terms each stay below 1e37 but whose sum would overflow
+    many = [base[i].copy() for i in range(len(base)) if i != light]
+    hot = base[light].copy()
+    for k in range(40):
+        h = hot.copy()
+        h["rad"] = 1.0
+        h["p"] = [12.0 + 2.0 * k, 70.0, 60.0 + (k % 5) * 6.0]
+        h["e"] = [7e35, 7e35, 7e35]
+        many.append(h)
+    many = np.array(many, dtype=base.dtype)
+    assert not jc.zero_exit_safe(many) and not _c_rule(many)
+    many["e"][len(base) - 1:] = 1.0
+    assert jc.zero_exit_safe(many) == _c_rule(many)
+    # random scenes around cornell: the two restatements agree on every one
+    rng = np.random.default_rng(7)
+    for t in range(300):
+        sp = base.copy()
+        k = rng.integers(0, len(sp))
+        which = rng.integers(0, 4)
+        if which == 0:
+            sp[k]["c"] = rng.choice([0.0, 0.5, -2e3, 999.0, 1e3, 1001.0], size=3)
+        elif which == 1:
+            sp[k]["e"] = rng.choice([0.0, 1.0, 1e30, 1e36, 1e37], size=3)
+        elif which == 2:
+            sp[k]["rad"] = rng.choice([0.0, 1e-3, 0.5, 16.5, 1e5])
+        else:
+            sp[k]["p"] = sp[k]["p"] + rng.normal(0, 20, 3)
+        assert jc.zero_exit_safe(sp) == _c_rule(sp), (t, sp[k])

@@ -1,0 +1,84 @@
+"""Spill guard for the precompiled kernels inside libbdpt.so (the instances that run when the
+scene-specialised build is off or unavailable, and the BVH instance N = -1 that always runs for
+large scenes).  The gfx950 code object is unpacked from the library's .hip_fatbin section and its
+kernel metadata read; every instance's VGPR spills, scratch size and SGPR spills must equal the
+recorded values below, so a register-pressure regression fails here on the CPU instead of showing
+up as a slower kernel on the GPU.  (tests/test_jit_codegen.py guards the specialised builds.)
+
+Recorded values and why they are acceptable:
+  * no instance spills VGPRs or uses scratch (private segment 0) -- including the BVH instance,
+    which earlier builds ran with 10 spilled VGPRs;
+  * the per-N instances hold the scene geometry in SGPRs (wave-uniform constant loads); from
+    N = 11 spheres the SGPR file (106) overflows by 2 per extra sphere and the excess goes to VGPR
+    lanes (v_writelane / v_readlane, no memory traffic).  These instances only run with
+    specialisation off: by default a <= 64-sphere scene runs its hipRTC build;
+  * the BVH instance keeps its traversal state in SGPRs and moves 6 (fused) / 8 (pass streams) of
+    them to VGPR lanes in the same way.
+"""
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import REPO
+
+LLVM = "/opt/rocm/lib/llvm/bin"
+LIB = os.path.join(REPO, "gpu_bidirectional_raytracer_amd", "libbdpt.so")
+sys.path.insert(0, os.path.join(REPO, "tools"))
+
+
+def _sgpr_spills(n, streams):
+    if n == -1:
+        return 8 if streams else 6
+    return 2 * (n - 10) if n > 10 else 0
+
+
+@pytest.fixture(scope="module")
+def kernels(tmp_path_factory):
+    if not os.path.exists(os.path.join(LLVM, "clang-offload-bundler")):
+        pytest.skip("no ROCm LLVM tools")
+    import jit_codegen_check as jc
+    d = tmp_path_factory.mktemp("co")
+    fat, co = str(d / "fat.bin"), str(d / "co.o")
+    subprocess.check_call([os.path.join(LLVM, "llvm-objcopy"), f"--dump-section=.hip_fatbin={fat}", LIB,
+                           str(d / "stripped.so")])
+    subprocess.check_call([os.path.join(LLVM, "clang-offload-bundler"), "--unbundle", "--type=o", f"--input={fat}",
+                           "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"])
+    notes = subprocess.check_output([os.path.join(LLVM, "llvm-readelf"), "--notes", co], text=True)
+    return {k["name"]: k for k in jc.kernel_notes(notes)}
+
+
+def test_every_instance_is_present(kernels):
+    for st in (0, 1):
+        for n in list(range(0, 17)) + [-1]:
+            name = f"_Z18bdpt_path_kernel_tIL{'i' if n >= 0 else 'in'}{abs(n)}ELb{st}EEv14bdpt_path_args"
+            assert name in kernels, name
+    for k in ("bdpt_mt607_kernel", "bdpt_light_kernel", "bdpt_accum_kernel", "bdpt_rand_planar_kernel",
+              "bdpt_pixels_kernel", "bdpt_frame_add_kernel"):
+        assert k in kernels, k
+
+
+def test_no_vgpr_spills_or_scratch(kernels):
+    for name, k in kernels.items():
+        assert k["vgpr_spill_count"] == 0, k
+        assert k["private_segment_fixed_size"] == 0, k
+
+
+def test_sgpr_spills_match_record(kernels):
+    for st in (0, 1):
+        for n in list(range(0, 17)) + [-1]:
+            name = f"_Z18bdpt_path_kernel_tIL{'i' if n >= 0 else 'in'}{abs(n)}ELb{st}EEv14bdpt_path_args"
+            assert kernels[name]["sgpr_spill_count"] == _sgpr_spills(n, st), kernels[name]
+    for k in ("bdpt_mt607_kernel", "bdpt_light_kernel", "bdpt_accum_kernel"):
+        assert kernels[k]["sgpr_spill_count"] == 0, kernels[k]
+
+
+def test_occupancy_of_the_path_instances(kernels):
+    """Every per-N instance fits 6 waves/SIMD (<= 80 VGPRs, 512 / 6 rounded down to 8) except the
+    >= 9-sphere fused ones, bounded at 5 (BDPT_FUSED_WAVES); the BVH instance fits 5 (<= 96)."""
+    for st in (0, 1):
+        for n in list(range(0, 17)) + [-1]:
+            name = f"_Z18bdpt_path_kernel_tIL{'i' if n >= 0 else 'in'}{abs(n)}ELb{st}EEv14bdpt_path_args"
+            bound = 96 if (n == -1 or (not st and n >= 9)) else 80
+            assert kernels[name]["vgpr_count"] <= bound, kernels[name]

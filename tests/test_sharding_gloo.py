@@ -1,5 +1,9 @@
-"""Multi-GPU path on CPU: world_size-2 gloo run of the band sharding + sum-reduce frame assembly
-(gpu_bidirectional_raytracer_amd.sharding), with the oracle rendering each rank's bands."""
+"""Multi-GPU path on CPU: world_size-2 gloo runs of the band sharding + sum-reduce frame assembly
+(gpu_bidirectional_raytracer_amd.sharding).  Each rank renders its own bands through the PRODUCT:
+a C-ABI context on the host-CPU backend (bdpt_create(..., BDPT_DEVICE_CPU)) with bdpt_set_shard,
+the same band rule the GPU kernel applies; every rank checks its ownership (rendered bands at the
+full count, zeros elsewhere) and rank 0 compares the reduced frame with the oracle's full frame bit
+for bit (4-row bands on cornell_glass, and bench.py's 8-row bands on cornell)."""
 import os
 import socket
 
@@ -25,43 +29,51 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, out_dir):
+def _worker(rank, world, port, out_dir, band, scene):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), BDPT_CPU_THREADS="2")
     import torch
     import torch.distributed as dist
+    import gpu_bidirectional_raytracer_amd as g
     import oracle
-    from golden.make_golden import read_scene_py  # noqa: E402
     from gpu_bidirectional_raytracer_amd import sharding as shd
 
     dist.init_process_group("gloo", rank=rank, world_size=world)
     scn = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "assets", "scenes",
-                       "cornell_glass.scn")
-    orig, target, sp = read_scene_py(scn)
-    W, H, band = 29, 37, 4
-    cam = oracle.update_camera(orig, target, W, H)
-    rnd = oracle.mt607(0)
-    lp = oracle.light_pass(sp, rnd, 0)
-    sid, vlp = [5, 77777, 123456, 4242424], [1, 1, 2, 2]
-    col = np.zeros((H, W, 3), np.float32)
-    cnt = np.zeros((H, W), np.uint32)
-    for y0, y1 in shd.owned_row_ranges(H, rank, world, band):
-        col, cnt, _ = oracle.path_passes(sp, rnd, cam, W, H, lp, sid, vlp, colors=col, counter=cnt,
-                                         rows=(y0, y1), nthreads=1)
+                       scene + ".scn")
+    W, H = 29, 37
+    cam, sp = g.read_scene(scn)
+    g.update_camera(cam, W, H)
+    s = g.PassScheduler()
+    s.light()
+    sid, vlp = s.next(4)
+    with g.Renderer(sp, W, H, cam, device=-1) as r:          # the product, host-CPU backend
+        r.set_shard(rank, world, band)
+        r.light_pass(0)
+        r.path_passes(sid, vlp)
+        col, cnt = r.read_radiance()
+    owned = (np.arange(H) // band) % world == rank
+    local_ok = (cnt[owned] == len(sid)).all() and (cnt[~owned] == 0).all() and (col[~owned] == 0).all()
     t_col = torch.from_numpy(col.reshape(-1).copy())
     t_cnt = torch.from_numpy(cnt.reshape(-1).astype(np.int32))
     shd.reduce_frame(t_col, t_cnt, dst=0)
+    flags = torch.tensor([int(local_ok)])
+    dist.all_reduce(flags, op=dist.ReduceOp.MIN)
     if rank == 0:
+        rnd = oracle.mt607(0)
+        lp = oracle.light_pass(sp, rnd, 0)
         full, fcnt, _ = oracle.path_passes(sp, rnd, cam, W, H, lp, sid, vlp, nthreads=1)
-        ok = np.array_equal(t_col.numpy().reshape(H, W, 3), full) and \
+        ok = bool(flags.item()) and np.array_equal(t_col.numpy().reshape(H, W, 3).view(np.uint32),
+                                                  full.view(np.uint32)) and \
             np.array_equal(t_cnt.numpy().reshape(H, W), fcnt.astype(np.int32))
         open(os.path.join(out_dir, "result"), "w").write("ok" if ok else "mismatch")
     dist.destroy_process_group()
 
 
-def test_gloo_world2_frame_assembly(tmp_path):
+@pytest.mark.parametrize("band,scene", [(4, "cornell_glass"), (8, "cornell")])
+def test_gloo_world2_frame_assembly(tmp_path, band, scene):
     torch = pytest.importorskip("torch")
     import torch.multiprocessing as mp
-    mp.spawn(_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    mp.spawn(_worker, args=(2, _free_port(), str(tmp_path), band, scene), nprocs=2, join=True)
     assert (tmp_path / "result").read_text() == "ok"

@@ -54,32 +54,51 @@ def jit_defines(spheres):
 
 
 def zero_exit_safe(spheres):
-    """bdpt_host.cpp jit_path_kernel's rule: some non-emitter is black, all scene values are finite
-    and colours <= 1e3, every emitter has e * 4 pi r^2 < 1e37 and keeps a gap >= max(1, 1e-4 *
-    scene scale) from every other sphere's surface."""
+    """Python restatement of bdpt_util.c bdpt_zero_exit_safe (the rule that decides
+    -DBDPT_JIT_ZERO_SAFE in bdpt_host.cpp jit_path_kernel): some non-emitter is black; all scene
+    values finite, every |c| <= 1e3 and every radius > 2^-16 * scene scale; every emitter keeps a
+    gap >= max(1, 1e-4 * scale) from every other sphere's surface; and the largest sum a vertex can
+    add after a black hit, n_lights * max(e * 4 pi r^2) * 1.1 + 0.5 * max|e| * max(1, max|c|) * g,
+    stays below 1e38 (g = the escaped-VLP normal-length factor 1 + 8 * 2^-24 * (|p| + r) / r)."""
     import math
-    vals = [float(v) for o in spheres for v in (o["rad"], *o["p"], *o["e"], *o["c"])]
-    if not all(math.isfinite(v) for v in vals) or any(float(v) > 1e3 for o in spheres for v in o["c"]):
+    n = len(spheres)
+    if n == 0:
         return False
-    if not any(not any(float(v) != 0.0 for v in o["e"]) and all(float(v) == 0.0 for v in o["c"])
-               for o in spheres):
-        return False
-    scale = max(math.hypot(*[float(v) for v in o["p"]]) + abs(float(o["rad"])) for o in spheres)
-    min_gap = max(1.0, 1e-4 * scale)
-    for i, e in enumerate(spheres):
-        if not any(float(v) != 0.0 for v in e["e"]):
-            continue
-        re = float(e["rad"])
-        if not max(abs(float(v)) for v in e["e"]) * 4.0 * math.pi * re * re < 1e37:
+    scale = cmax = emax = nee = 0.0
+    g = 1.0
+    black = False
+    for o in spheres:
+        v = [float(x) for x in (o["rad"], *o["p"], *o["e"], *o["c"])]
+        if not all(math.isfinite(x) for x in v):
             return False
+        scale = max(scale, math.sqrt(v[1] * v[1] + v[2] * v[2] + v[3] * v[3]) + abs(v[0]))
+        cmax = max(cmax, *(abs(x) for x in v[7:10]))
+        emits = any(x != 0.0 for x in v[4:7])
+        if not emits and all(x == 0.0 for x in v[7:10]):
+            black = True
+    if not black or not cmax <= 1e3:
+        return False
+    min_gap, min_rad = max(1.0, 1e-4 * scale), math.ldexp(scale, -16)
+    for i, e in enumerate(spheres):
+        re = abs(float(e["rad"]))
+        if not re > min_rad:
+            return False
+        ev = [float(x) for x in e["e"]]
+        if not any(x != 0.0 for x in ev):
+            continue
+        em = max(abs(x) for x in ev)
+        emax = max(emax, em)
+        nee += em * 4.0 * math.pi * re * re
+        pn = math.sqrt(sum(float(x) * float(x) for x in e["p"]))
+        g = max(g, 1.0 + 8.0 * math.ldexp(pn + re, -24) / re)
         for k, o in enumerate(spheres):
             if k == i:
                 continue
-            ro = float(o["rad"])
-            d = math.dist([float(v) for v in e["p"]], [float(v) for v in o["p"]])
+            ro = abs(float(o["rad"]))
+            d = math.sqrt(sum((float(a) - float(b)) ** 2 for a, b in zip(e["p"], o["p"])))
             if not max(d - re - ro, ro - d - re, re - d - ro) >= min_gap:
                 return False
-    return True
+    return nee * 1.1 + 0.5 * emax * max(1.0, cmax) * g < 1e38
 
 
 def scalar_writes(asm):
@@ -129,7 +148,8 @@ def build(scene, waves, workdir, extra=()):
 def kernel_notes(notes):
     kernels, cur = [], None
     for line in notes.splitlines():
-        m = re.match(r"\s*\.(name|vgpr_count|sgpr_count|vgpr_spill_count|sgpr_spill_count):\s+(\S+)", line)
+        m = re.match(r"\s*\.(name|vgpr_count|sgpr_count|vgpr_spill_count|sgpr_spill_count|"
+                     r"private_segment_fixed_size):\s+(\S+)", line)
         if not m:
             continue
         if m.group(1) == "name":
