@@ -483,6 +483,18 @@ static hipFunction_t jit_build(bdpt_ctx* c, const std::string& name, const std::
     return fn;
 }
 
+// Passes per launch of the fused S = 1 kernel.  Its workgroups stage a VLP (48 B) and a sid per
+// pass of the launch in LDS: 128 passes make 31.5 KB per workgroup and cap a CU at 5 workgroups
+// (5 waves/SIMD); 64 passes (with the 2-KB sincos table) fit 6.  BDPT_FUSED_MAX_PASSES overrides.
+static int fused_max_passes() {
+    static const int cap = [] {
+        const char* e = getenv("BDPT_FUSED_MAX_PASSES");
+        const int v = e ? atoi(e) : 64;
+        return v < 1 ? 1 : (v > 128 ? 128 : v);
+    }();
+    return cap;
+}
+
 // The specialised kernel for the context's scene and pass-stream mode, compiled on first use;
 // nullptr = use the precompiled instance (reason in c->jit_err).
 static hipFunction_t jit_path_kernel(bdpt_ctx* c, bool streams) {
@@ -521,7 +533,9 @@ static hipFunction_t jit_path_kernel(bdpt_ctx* c, bool streams) {
     // Black-surface exit (bdpt_kernels.hip BDPT_ZERO_EXIT): compiled in only when ending a path at
     // a black non-emitter is provably exact for this scene (bdpt_util.c bdpt_zero_exit_safe).
     const bool zero_exit = bdpt_zero_exit_safe(c->spheres.data(), n) != 0;
-    const char* wenv = getenv("BDPT_JIT_WAVES");
+    // Waves/SIMD the build targets.  The fused S = 1 kernel too starts at 6 (its LDS is sized for
+    // 6 workgroups per CU below): caustic's fused build takes 79 VGPRs, within the 80 of 6 waves.
+    const char* wenv = getenv(streams ? "BDPT_JIT_WAVES" : "BDPT_JIT_FUSED_WAVES");
     int waves = wenv ? atoi(wenv) : 6;
     const std::string name = "&bdpt_path_kernel_t<" + std::to_string(n) + (streams ? ", true>" : ", false>");
     const char* jflags = getenv("BDPT_JIT_FLAGS");
@@ -536,6 +550,7 @@ static hipFunction_t jit_path_kernel(bdpt_ctx* c, bool streams) {
             "-DBDPT_JIT_ZERO_SAFE=" + std::to_string(zero_exit ? 1 : 0),
             "-DBDPT_WAVES_PER_SIMD=" + std::to_string(waves)};
         std::vector<std::string> all = opts;
+        if (!streams) all.push_back("-DBDPT_FUSED_WAVES=" + std::to_string(waves));
         if (const char* extra = getenv("BDPT_JIT_FLAGS")) {    // experiments: extra -D options
             std::string tok;
             for (const char* q = extra;; q++) {
@@ -552,12 +567,14 @@ static hipFunction_t jit_path_kernel(bdpt_ctx* c, bool streams) {
         hipFunction_t fn = jit_build(c, name, all);
         if (!fn) return nullptr;
         // The 4-KB sincos table costs a workgroup per CU when LDS bounds the count (large
-        // scenes: 16 B per sphere); then take the 2-KB table of even entries (bdpt_math.h).
-        // Estimated with one pass slot (bdpt_path_passes' smem formula).
+        // scenes: 16 B per sphere; the fused kernel: a VLP and a sid per pass of the launch);
+        // then take the 2-KB table of even entries (bdpt_math.h).  Estimated with bdpt_path_passes'
+        // smem formula: one pass slot for the pass-stream kernel, fused_max_passes() for the fused.
         int stat = 0;
         if (!coarse && !user_coarse &&
             hipFuncGetAttribute(&stat, HIP_FUNC_ATTRIBUTE_SHARED_SIZE_BYTES, fn) == hipSuccess) {
-            const size_t dyn = sizeof(float4) * (4 * (size_t)n + 3 + 5 + 4 * 128 * 2) + sizeof(unsigned);
+            const size_t slots = streams ? 1 : (size_t)fused_max_passes();
+            const size_t dyn = sizeof(float4) * (4 * (size_t)n + 3 * slots + 5 + 4 * 128 * 2) + sizeof(unsigned) * slots;
             const size_t lds = 160 * 1024, fine = lds / (dyn + stat), half = lds / (dyn + stat - 2048);
             if (fine < (size_t)waves && half > fine) {
                 coarse = true;
@@ -1012,6 +1029,7 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
     if (S > chunk) S = chunk;
     if (S > npass) S = npass;
     if (S < 1) S = 1;
+    if (S == 1 && chunk > fused_max_passes()) chunk = fused_max_passes();   // fused: LDS per pass
     c->last_streams = S;
     const bool bvh = c->has_bvh && (c->traversal == BDPT_TRAVERSE_BVH ||
                                     (c->traversal == BDPT_TRAVERSE_AUTO && c->bvh_ns >= kBvhAutoSpheres));

@@ -52,11 +52,15 @@ BDPT_HD void bdpt_sincos_dp(double x, double* so, double* co) {
 // sin x = S_k cos r + C_k sin r, cos x = C_k cos r - S_k sin r with S_k = sintab[k] =
 // sin(2pi k/N) and C_k = cos(2pi k/N) = sintab[(k + N/4) mod N] (bdpt_sincos_table.h, N = 512,
 // correctly rounded, so the two are the same double; the four axis entries exact).  With
-// |r| <= pi/512 the Taylor terms r^7/7! and r^6/6! are below 2^-56 relative and are dropped
-// (sin r = r - r^3/6 + r^5/120, cos r = 1 - r^2/2 + r^4/24).  For 0 <= x <= 2pi (the render
-// path's x = 2pi u).  BDPT_SC_COARSE = 1: the even entries only (N = 256, 2 KB of LDS instead of
-// 4 KB, for kernels whose LDS bounds the workgroups per CU); then r^6/6! is kept in cos r.  Same
-// exhaustive check as bdpt_sincos_dp for both (tests/test_math.py).
+// |r| <= pi/512 the Taylor terms r^7/7! and r^6/6! are dropped (sin r = r - r^3/6 + r^5/120,
+// cos r = 1 - r^2/2 + r^4/24).  The dropped sine term is below 2^-61 relative, but r^6/6! reaches
+// 7.4e-17 = 2^-53.6 -- about 0.67 ulp of cos r ~ 1 -- so the fp64 cos r is NOT accurate to a few
+// ulp by this argument alone, and no error bound is claimed here: exactness of the float results
+// rests on the exhaustive test (every float x = 2pi u the render path can pass, both tables,
+// tests/test_math.py), which must be re-run after any edit to the table, the reduction or the
+// polynomials.  For 0 <= x <= 2pi (the render path's x = 2pi u).  BDPT_SC_COARSE = 1: the even
+// entries only (N = 256, 2 KB of LDS instead of 4 KB, for kernels whose LDS bounds the
+// workgroups per CU); then r^6/6! is kept in cos r.
 #ifndef BDPT_SC_COARSE
 #define BDPT_SC_COARSE 0
 #endif

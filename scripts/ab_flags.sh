@@ -16,7 +16,7 @@ for r in $(seq 1 ${ROUNDS:-2}); do
       env $v timeout -k 10 300 python bench.py --no-cpu-baseline --scene $sc ${BENCH_ARGS:-} > gpurun_out/abf_$k.log 2>&1
       rc=$?
       if [ $rc -ne 0 ]; then echo "STOP [$v] $sc rc=$rc"; tail -5 gpurun_out/abf_$k.log; exit $rc; fi
-      echo "round $r $sc [${v:-default}] $(python -c "import json; d=json.loads(open('gpurun_out/abf_$k.log').read().strip().splitlines()[-1]); print(d['value'], d['device_ms_per_step'], d['config']['specialized'], 'S=%d' % d['config']['pass_streams'], 'k=%.3f' % d['roofline']['avg_launch_ms'])")"
+      echo "round $r $sc [${v:-default}] $(python -c "import json; d=json.loads(open('gpurun_out/abf_$k.log').read().strip().splitlines()[-1]); r=d['roofline'] or {}; print(d['value'], d['device_ms_per_step'], d['config']['specialized'], 'S=%d' % d['config']['pass_streams'], 'k=%s' % r.get('avg_launch_ms'))")"
     done
   done
 done

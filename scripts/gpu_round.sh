@@ -49,6 +49,17 @@ for s in $STEPS; do
       timeout -k 10 400 python bench.py --workload $w --cpu-seconds 6 > gpurun_out/wl_$w.log 2>&1
       rc=$?; echo "workload $w rc=$rc"; tail -1 gpurun_out/wl_$w.log | cut -c1-400; ok_or_stop $rc wl_$w
     done ;;
+  inproc)
+    # bench.py --gpus N without torchrun: one in-process multi-device context (rehearsed on one
+    # GPU with --devices 0,0: two shards, peer-copy reduce), then --gpus 2 must refuse on 1 GPU
+    timeout -k 10 300 python bench.py --gpus 2 --devices 0,0 --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/inproc.log 2>&1
+    rc=$?; tail -1 gpurun_out/inproc.log | cut -c1-600; ok_or_stop $rc inproc
+    timeout -k 10 120 python bench.py --gpus 2 --steps 2 > gpurun_out/refuse.log 2>&1
+    rc=$?; echo "--gpus 2 on this box: exit $rc: $(tail -1 gpurun_out/refuse.log)"
+    [ $rc -eq 1 ] || { echo "STOP refuse (expected exit 1)"; exit 3; } ;;
+  profile)
+    timeout -k 10 1500 bash scripts/profile_workloads.sh > gpurun_out/profile.log 2>&1
+    rc=$?; tail -20 gpurun_out/profile.log; ok_or_stop $rc profile ;;
   shard)
     timeout -k 10 400 python scripts/shard_probe.py ${SHARD_ARGS:-} > gpurun_out/shard_probe.log 2>&1
     rc=$?; cat gpurun_out/shard_probe.log | tail -12; ok_or_stop $rc shard ;;

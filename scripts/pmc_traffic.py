@@ -11,6 +11,7 @@ import csv, glob, json, os, sys
 
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
 out = sys.argv[2] if len(sys.argv) > 2 else "profiles/pmc_traffic.json"
+pat = sys.argv[3] if len(sys.argv) > 3 else "pmc*"          # the PMC runs of one workload
 
 
 def counter(pattern, kernel, name):
@@ -22,8 +23,8 @@ def counter(pattern, kernel, name):
     return sum(vals) / len(vals) if vals else None, len(vals)
 
 
-fetch, nd = counter("pmc*", "path_kernel", "FETCH_SIZE")
-write, _ = counter("pmc*", "path_kernel", "WRITE_SIZE")
+fetch, nd = counter(pat, "path_kernel", "FETCH_SIZE")
+write, _ = counter(pat, "path_kernel", "WRITE_SIZE")
 known = {}
 kb = os.path.join(root, "calib_bytes.jsonl")
 if os.path.exists(kb):
@@ -46,11 +47,15 @@ for k, c in calib.items():
             c["line_bytes_per_reported"] = round(c["line_bytes"] / c["fetch_reported"], 4)
     if c.get("write_reported"):
         c["write_bytes_per_reported"] = round(c["write_bytes"] / c["write_reported"], 4)
+if not calib and os.path.exists(out):                      # no calibration run: reuse the recorded one
+    prev = json.load(open(out))
+    prev = [prev] if "scene" in prev else list(prev.values())
+    calib = next((p_["calibration"] for p_ in prev if p_.get("calibration")), {})
 fscale = calib.get("gather20", {}).get("line_bytes_per_reported")
 wscale = calib.get("store12", {}).get("write_bytes_per_reported")
 # the workload of the PMC runs: their own bench.py JSON line
 cfg, roof = {}, {}
-for f in sorted(glob.glob(os.path.join(root, "pmc*.log"))):
+for f in sorted(glob.glob(os.path.join(root, pat + ".log"))):
     lines = [l for l in open(f) if l.startswith("{")]
     if lines:
         d = json.loads(lines[-1])

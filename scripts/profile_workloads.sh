@@ -1,0 +1,34 @@
+#!/bin/bash
+# Per-workload profiles on the GPU box: for each bench.py workload, one rocprofv3 kernel-trace
+# --stats run of the default bench command and the PMC passes (separate runs, MI355X_MICROARCH.md
+# "HBM") with the pass-stream mode the default run settles on (-1: one pass per lane, 1: fused).
+#   WORKLOADS="cornell1080:-1 caustic8:1 weak64:-1" bash scripts/profile_workloads.sh
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out; export TMPDIR=/tmp
+export BDPT_JIT_CACHE=$(mktemp -d /tmp/bdpt-jit-prof.XXXXXX)     # one compile per scene, shared
+stop() { echo "STOP $1 (exit $2)"; exit "$2"; }
+PMC_SETS=(
+  "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM GRBM_GUI_ACTIVE"
+  "SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT"
+  "FETCH_SIZE"
+  "WRITE_SIZE"
+  "TCC_HIT_sum TCC_MISS_sum"
+)
+for ws in ${WORKLOADS:-cornell1080:-1 caustic8:1 weak64:-1}; do
+  w=${ws%%:*}; S=${ws##*:}
+  steps=${STEPS_STATS:-10}
+  [ "$w" = weak64 ] && steps=${STEPS_STATS64:-6}
+  rm -rf gpurun_out/prof_$w
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$w -o run --output-format csv -- \
+      python3 bench.py --workload $w --no-cpu-baseline --steps $steps --warmup 3 > gpurun_out/prof_$w.log 2>&1 || stop "stats $w" $?
+  echo "stats $w: $(grep '^{' gpurun_out/prof_$w.log | tail -1 | cut -c1-200)"
+  i=0
+  for set in "${PMC_SETS[@]}"; do
+    i=$((i+1)); rm -rf gpurun_out/pmc_${w}_$i
+    timeout -s KILL 240 rocprofv3 --pmc $set --kernel-trace -d gpurun_out/pmc_${w}_$i -o run --output-format csv -- \
+        python3 bench.py --workload $w --no-cpu-baseline --no-smt-probe --steps 4 --warmup 1 --streams $S > gpurun_out/pmc_${w}_$i.log 2>&1 || stop "pmc $w $i" $?
+    echo "pmc $w set $i ok"
+  done
+done
+echo PROFILE_DONE
