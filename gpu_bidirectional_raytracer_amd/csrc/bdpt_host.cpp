@@ -484,8 +484,10 @@ static hipFunction_t jit_build(bdpt_ctx* c, const std::string& name, const std::
 }
 
 // Passes per launch of the fused S = 1 kernel.  Its workgroups stage a VLP (48 B) and a sid per
-// pass of the launch in LDS: 128 passes make 31.5 KB per workgroup and cap a CU at 5 workgroups
-// (5 waves/SIMD); 64 passes (with the 2-KB sincos table) fit 6.  BDPT_FUSED_MAX_PASSES overrides.
+// pass of the launch in LDS: 128 passes make 31.5 KB per workgroup.  Measured on caustic8 (one
+// session, two rounds, profiles/r03_s1_ab_fused.txt): 64 passes at 5 waves/SIMD (4-KB sincos
+// table) 48.8 Gs/s, 64 at 6 (2-KB table) 48.55, 128 at 6 48.2, 128 at 5 (round 2) 47.9.
+// BDPT_FUSED_MAX_PASSES overrides.
 static int fused_max_passes() {
     static const int cap = [] {
         const char* e = getenv("BDPT_FUSED_MAX_PASSES");
@@ -533,10 +535,11 @@ static hipFunction_t jit_path_kernel(bdpt_ctx* c, bool streams) {
     // Black-surface exit (bdpt_kernels.hip BDPT_ZERO_EXIT): compiled in only when ending a path at
     // a black non-emitter is provably exact for this scene (bdpt_util.c bdpt_zero_exit_safe).
     const bool zero_exit = bdpt_zero_exit_safe(c->spheres.data(), n) != 0;
-    // Waves/SIMD the build targets.  The fused S = 1 kernel too starts at 6 (its LDS is sized for
-    // 6 workgroups per CU below): caustic's fused build takes 79 VGPRs, within the 80 of 6 waves.
+    // Waves/SIMD the build targets: 6 for the pass-stream kernel, 5 for the fused S = 1 kernel
+    // (at 6 it fits without spills, but then the LDS formula below takes the 2-KB sincos table and
+    // caustic8 measured 0.6 % slower than 5 waves with the 4-KB table; fused_max_passes()).
     const char* wenv = getenv(streams ? "BDPT_JIT_WAVES" : "BDPT_JIT_FUSED_WAVES");
-    int waves = wenv ? atoi(wenv) : 6;
+    int waves = wenv ? atoi(wenv) : (streams ? 6 : 5);
     const std::string name = "&bdpt_path_kernel_t<" + std::to_string(n) + (streams ? ", true>" : ", false>");
     const char* jflags = getenv("BDPT_JIT_FLAGS");
     const bool user_coarse = jflags && strstr(jflags, "BDPT_SC_COARSE");   // experiments decide
