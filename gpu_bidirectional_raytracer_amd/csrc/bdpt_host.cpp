@@ -1033,6 +1033,12 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
     if (S > npass) S = npass;
     if (S < 1) S = 1;
     if (S == 1 && chunk > fused_max_passes()) chunk = fused_max_passes();   // fused: LDS per pass
+    // equal launches: 128 passes over a 4097 x 513-row band (chunk 126) are 2 x 64, not 126 + 2
+    if (npass > chunk) {
+        const int nch = (npass + chunk - 1) / chunk;
+        chunk = (npass + nch - 1) / nch;
+        if (S > chunk) S = chunk;
+    }
     c->last_streams = S;
     const bool bvh = c->has_bvh && (c->traversal == BDPT_TRAVERSE_BVH ||
                                     (c->traversal == BDPT_TRAVERSE_AUTO && c->bvh_ns >= kBvhAutoSpheres));

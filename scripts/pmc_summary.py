@@ -27,11 +27,16 @@ print(f"FETCH (MB) / WRITE (MB)     {g('FETCH_SIZE') / 1024:.1f} / {g('WRITE_SIZ
 # figures plus the bench configuration of the PMC runs, read by bench.py into its `valu` object
 if len(sys.argv) > 4:
     import json
-    cfg = {}
+    cfg, ppl = {}, None
     for f in sorted(glob.glob(os.path.join(root, pat + ".log"))):
         lines = [l for l in open(f) if l.startswith("{")]
         if lines:
-            cfg = json.loads(lines[-1])["config"]
+            d = json.loads(lines[-1])
+            cfg = d["config"]
+            # passes per launch as the bench measured it (the fused kernel splits a step into
+            # launches of at most 64 passes), as bench.py matches it
+            nl = (d.get("roofline") or {}).get("launches")
+            ppl = cfg.get("passes_per_step") * d["steps"] / nl if nl else cfg.get("passes_per_step")
             break
     rec = {"workload": cfg.get("workload", "cornell1080").split(":")[0],
            "valu_busy": round(g('SQ_INSTS_VALU') * 2 / (4 * 256 * cyc), 4),
@@ -43,7 +48,7 @@ if len(sys.argv) > 4:
            "valu_insts_per_wave": round(g('SQ_INSTS_VALU') / g('SQ_WAVES'), 1),
            "fetch_reported_kib": g('FETCH_SIZE'), "write_reported_kib": g('WRITE_SIZE'),
            "scene": cfg.get("scene"), "width": cfg.get("width"), "height": cfg.get("height"),
-           "passes_per_launch": cfg.get("passes_per_step"), "pass_streams": cfg.get("pass_streams"), "specialized": cfg.get("specialized", False),
+           "passes_per_launch": ppl, "pass_streams": cfg.get("pass_streams"), "specialized": cfg.get("specialized", False),
            "source": "rocprofv3 --pmc SQ_INSTS_VALU / SQ_THREAD_CYCLES_VALU / SQ_ACTIVE_INST_VALU / "
                      "GRBM_GUI_ACTIVE / TCC_HIT_sum / TCC_MISS_sum (separate passes), scripts/pmc_summary.py"}
     rec = {k: (None if isinstance(v, float) and v != v else v) for k, v in rec.items()}   # NaN -> null

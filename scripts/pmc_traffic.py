@@ -54,15 +54,17 @@ if not calib and os.path.exists(out):                      # no calibration run:
 fscale = calib.get("gather20", {}).get("line_bytes_per_reported")
 wscale = calib.get("store12", {}).get("write_bytes_per_reported")
 # the workload of the PMC runs: their own bench.py JSON line
-cfg, roof = {}, {}
+cfg, roof, ppl = {}, {}, 16
 for f in sorted(glob.glob(os.path.join(root, pat + ".log"))):
     lines = [l for l in open(f) if l.startswith("{")]
     if lines:
         d = json.loads(lines[-1])
         cfg, roof = d["config"], d.get("roofline") or {}
+        nl = roof.get("launches")                         # passes per launch as bench.py measures it
+        ppl = cfg.get("passes_per_step", 16) * d["steps"] / nl if nl else cfg.get("passes_per_step", 16)
         break
 rec = {"workload": cfg.get("workload", "cornell1080").split(":")[0], "scene": cfg.get("scene", "cornell"), "width": cfg.get("width", 1921), "height": cfg.get("height", 1081),
-       "passes_per_launch": float(cfg.get("passes_per_step", 16)), "pass_streams": cfg.get("pass_streams"), "specialized": cfg.get("specialized", False),
+       "passes_per_launch": float(ppl), "pass_streams": cfg.get("pass_streams"), "specialized": cfg.get("specialized", False),
        "fetch_reported_bytes_per_launch": int(fetch), "write_reported_bytes_per_launch": int(write),
        "fetch_scale": fscale, "write_scale": wscale,
        "hbm_bytes_per_launch": int(fetch * (fscale or 1.0) + write * (wscale or 1.0)),

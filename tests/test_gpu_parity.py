@@ -175,7 +175,8 @@ def test_pass_streams_bit_exact(gpu, rnd0, streams):
 
 
 def test_per_lane_streams_policy(gpu):
-    """-1: one pass per lane (S = passes in the launch, <= 128); 1 forces the fused kernel."""
+    """-1: one pass per lane (S = passes in the launch, <= 128, launches of equal size); 1 forces
+    the fused kernel."""
     r, _, _ = make("cornell", 1921, 1081, gpu)
     r.set_streams(-1)
     sid, vlp = schedule(200)
@@ -183,7 +184,9 @@ def test_per_lane_streams_policy(gpu):
     assert r.last_streams == 1
     r.path_passes(sid[1:9], vlp[1:9])
     assert r.last_streams == 8
-    r.path_passes(sid[9:200], vlp[9:200])                 # 128 + 63 passes in two launches
+    r.path_passes(sid[9:200], vlp[9:200])                 # 191 passes: launches of 96 + 95
+    assert r.last_streams == 96
+    r.path_passes(sid[:128], vlp[:128])                   # 128 passes: one launch
     assert r.last_streams == 128
     r.set_shard(3, 8, 8)
     r.path_passes(sid[:8], vlp[:8])
