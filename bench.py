@@ -406,6 +406,8 @@ def main():
     for k in range(args.warmup):
         step(k)
     r.synchronize()
+    if mode == "inproc":                                      # RCCL's first-use set-up, untimed
+        r.reduce_frame()
     r.path_timing(reset=True)
     r.kernel_timing(reset=True)
 
@@ -413,6 +415,10 @@ def main():
     t_col = t_cnt = None
     if dist is not None:
         t_col, t_cnt = shd.device_tensors(r, f"cuda:{local}")
+        # one reduce of the same sizes on scratch buffers before the clock starts, so the timed
+        # reduce does not pay RCCL's first-use set-up (channels, buffers) for these sizes
+        shd.reduce_frame(torch.zeros_like(t_col), torch.zeros_like(t_cnt), dst=0)
+        torch.cuda.synchronize()
 
     barrier()
     torch.cuda.synchronize()
@@ -497,7 +503,7 @@ def main():
                                r.last_streams, r.last_specialized) if single else None
             if vrec:
                 for k in ("valu_busy", "valu_lane_utilisation", "wait_frac", "issue_stall_frac", "active_frac",
-                          "valu_insts_per_wave", "l2_hit_rate"):
+                          "valu_insts_per_wave", "l2_hit_rate", "valu_issue_occupancy"):
                     if k in vrec:
                         roofline[{"valu_busy": "valu_busy_pmc",
                                   "valu_lane_utilisation": "lane_utilisation_pmc"}.get(k, k + "_pmc")] = vrec[k]

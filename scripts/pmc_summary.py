@@ -51,6 +51,12 @@ if len(sys.argv) > 4:
            "passes_per_launch": ppl, "pass_streams": cfg.get("pass_streams"), "specialized": cfg.get("specialized", False),
            "source": "rocprofv3 --pmc SQ_INSTS_VALU / SQ_THREAD_CYCLES_VALU / SQ_ACTIVE_INST_VALU / "
                      "GRBM_GUI_ACTIVE / TCC_HIT_sum / TCC_MISS_sum (separate passes), scripts/pmc_summary.py"}
+    # issue-weighted VALU occupancy when the instruction-mix passes ran (scripts/valu_weighted.py)
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import valu_weighted
+    wv = valu_weighted.weighted(m, valu_weighted.issue_rates())
+    if wv:
+        rec["valu_issue_occupancy"] = [round(wv[1], 4), round(wv[2], 4)]
     rec = {k: (None if isinstance(v, float) and v != v else v) for k, v in rec.items()}   # NaN -> null
     out = sys.argv[4]
     data = json.load(open(out)) if os.path.exists(out) else {}

@@ -1,7 +1,8 @@
 #!/bin/bash
 # Per-workload profiles on the GPU box: for each bench.py workload, one rocprofv3 kernel-trace
 # --stats run of the default bench command and the PMC passes (separate runs, MI355X_MICROARCH.md
-# "HBM") with the pass-stream mode the default run settles on (-1: one pass per lane, 1: fused).
+# "HBM") with the pass-stream mode the default run settles on (-1: one pass per lane, 1: fused);
+# the last two passes split the VALU instructions by class (scripts/valu_weighted.py).
 #   WORKLOADS="cornell1080:-1 caustic8:1 weak64:-1" bash scripts/profile_workloads.sh
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -14,6 +15,8 @@ PMC_SETS=(
   "FETCH_SIZE"
   "WRITE_SIZE"
   "TCC_HIT_sum TCC_MISS_sum"
+  "SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 GRBM_GUI_ACTIVE"
+  "SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE"
 )
 for ws in ${WORKLOADS:-cornell1080:-1 caustic8:1 weak64:-1}; do
   w=${ws%%:*}; S=${ws##*:}
