@@ -46,7 +46,9 @@ def weighted(m, r):
     rest = m["SQ_INSTS_VALU"] - (f32 + trans + dp + i32 + other_half)
     simd_cycles = 256 * 4 * m["GRBM_GUI_ACTIVE"] / 8      # 1024 SIMDs x kernel cycles (per XCD)
     fixed = f32 * r["full"] + trans * r["quarter"] + dp * r["f64"] + other_half * r["half"]
-    lo = (fixed + (i32 + rest) * r["full"]) / simd_cycles
+    # (both clamped at 1: the costs were measured at 8 waves/SIMD, where an issue slot is contended
+    # a little more than at the kernels' 5-6, so a fully busy SIMD can price slightly above 1)
+    lo = min(1.0, (fixed + (i32 + rest) * r["full"]) / simd_cycles)
     hi = min(1.0, (fixed + (i32 + rest) * r["half"]) / simd_cycles)
     classes = (("fp32 add/mul/fma (full rate)", f32), ("fp32 sqrt/rcp (quarter)", trans),
                ("fp64 add/mul/fma (half)", dp), ("int32 (full..half)", i32),

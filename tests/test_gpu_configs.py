@@ -10,8 +10,8 @@ configs[3] caustic 1921x1081, 4096 spp on 8 pixel-band shards -> shard sum == on
            summed frame (68 rows, 6 %) + the last row vs the oracle
 configs[4] synthetic64 4097x4097 -> one 4097x512 band (what one of 8 GPUs renders) at the
            full 8192 spp (vlp_index wraps inside the run): ownership and counters over the frame;
-           a whole 8-row tile band in the middle of the GPU's band, and its first and last rows,
-           vs the oracle (10 of 512 rows)
+           whole 8-row tile bands at the start, middle and end of the GPU's band vs the oracle
+           (24 of 512 rows)
 """
 import os
 
@@ -119,8 +119,8 @@ def test_config4_synthetic64_4097_band_8192spp(gpu, rnd0):
     """configs[4] as one GPU of the 8-GPU weak-scaling run renders it (bench.py --workload weak64):
     the 64-sphere synthetic scene at 4097x4097, one 4097x512 band (rank 3 of 8 fixed bands), the
     full 8192 spp -- so vlp_index wraps past LIGHT_POINTS inside the run (pass 8190, SURVEY
-    Appendix A.3).  Counters and ownership over the frame, oracle spot checks on 4 pixel spans
-    at the full spp."""
+    Appendix A.3).  Counters and ownership over the frame; the band's first, middle and last 8-row
+    tile bands vs the oracle at the full spp."""
     W, H, spp, N, rank, band = 4097, 4097, 8192, 8, 3, 512
     r, cam, sp = _setup("synthetic64", W, H, gpu)
     assert len(sp) == 64
@@ -135,8 +135,8 @@ def test_config4_synthetic64_4097_band_8192spp(gpu, rnd0):
     _pixels_are_toint(r, col)
     lp = oracle.light_pass(sp, rnd0, 0)
     y0 = rank * band
-    mid = y0 + band // 2                                   # a whole 8-row tile band, mid-band
-    for rows in ((mid, mid + 8), (y0, y0 + 1), (y0 + band - 1, y0 + band)):
+    mid = y0 + band // 2                                   # whole 8-row tile bands: start, middle, end
+    for rows in ((y0, y0 + 8), (mid, mid + 8), (y0 + band - 8, y0 + band)):
         ocol, ocnt, _ = oracle.path_passes(sp, rnd0, cam, W, H, lp, sid, vlp, rows=rows)
         _same(col[rows[0]:rows[1]], ocol[rows[0]:rows[1]], f"rows {rows}")
         _same(cnt[rows[0]:rows[1]], ocnt[rows[0]:rows[1]], f"rows {rows} counters")
