@@ -266,6 +266,15 @@ __device__ __forceinline__ f3 cosine_tail(f3 w, f3 u, float u_phi, float u_r2, f
 #define BDPT_PACK_EDGES 1
 #endif
 // camera terms: per-lane fp64 base in LDS, kz products formed once per workgroup
+// Fused S = 1 kernel: a lane whose path ends parks until at least BDPT_REGEN_K lanes of its wave
+// (or all of its live lanes) are parked; then they start their next passes together, so the
+// camera-ray and path-start code runs for groups of lanes instead of a few lanes in almost every
+// iteration.  1 = restart at once (no parking); 64 = whole-wave lockstep.  One-session A/B
+// (profiles/r03_s13_ab_regen.txt): caustic8 48.5 -> 52.3 Gs/s (+7.8 %) at 48, the same within
+// 0.5 % for 16..56, 49.1 at 64; open +2 to +3.5 %, simple +1 %, cornell (fused) +10 %.
+#ifndef BDPT_REGEN_K
+#define BDPT_REGEN_K 48
+#endif
 #ifndef BDPT_CAMB
 #define BDPT_CAMB 1
 #endif
@@ -768,7 +777,7 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
 #endif
     load_rand5(rnd, j, q0, q1, q2, q3, q4);
     f3 ro = mk(0.f, 0.f, 0.f), rd = ro, thr = ro, rad = ro, nl = ro;
-    bool specular = true, fresh = true;
+    bool specular = true, fresh = true, parked = false;
     bool alive = active && nslot > 0 && cnt0 + (unsigned)s0 < BDPT_DEV_COUNTER_CAP;
 
     while (__builtin_amdgcn_ballot_w64(alive) != 0) {                   // wave-uniform loop
@@ -1316,6 +1325,10 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                 depth = 0;
                 const int pn = s0 + k * S;
                 alive = pn < a.npass && cnt0 + (unsigned)pn < BDPT_DEV_COUNTER_CAP;
+                if constexpr (!STREAMS && BDPT_REGEN_K > 1) {
+                    parked = alive;
+                    alive = false;
+                }
             }
             if (alive) {                  // prefetch the next segment's random numbers (:619)
                 // 26 + 25 i and the pass's sid are rebuilt here rather than kept live across the
@@ -1330,6 +1343,20 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                 else
 #endif
                 load_rand5(rnd, j, q0, q1, q2, q3, q4);
+            }
+        }
+        if constexpr (!STREAMS && BDPT_REGEN_K > 1) {
+            // release the parked lanes together (wave-uniform decision)
+            const unsigned long long mp = __builtin_amdgcn_ballot_w64(parked);
+            if (mp != 0 && (__popcll(mp) >= BDPT_REGEN_K || __builtin_amdgcn_ballot_w64(alive) == 0)) {
+                if (parked) {
+                    parked = false;
+                    alive = true;
+                    unsigned xyv = xy;
+                    asm volatile("" : "+v"(xyv));
+                    const unsigned li = (xyv >> 16) * (unsigned)a.W + (xyv & 0xffffu);
+                    load_rand5(rnd, (26u + li * 25u + SID[k]) % M5, q0, q1, q2, q3, q4);
+                }
             }
         }
         BDPT_TICK(5);                 // path end / accumulation / RNG prefetch
