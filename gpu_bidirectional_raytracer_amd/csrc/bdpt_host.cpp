@@ -1039,9 +1039,14 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
         chunk = (npass + nch - 1) / nch;
         if (S > chunk) S = chunk;
     }
-    c->last_streams = S;
     const bool bvh = c->has_bvh && (c->traversal == BDPT_TRAVERSE_BVH ||
                                     (c->traversal == BDPT_TRAVERSE_AUTO && c->bvh_ns >= kBvhAutoSpheres));
+    // auto: the pass-stream kernel renders two passes per lane in launches of >= 4 passes (lanes
+    // whose first path ends early start the second in groups, bdpt_kernels.hip BDPT_REGEN_STREAMS):
+    // cornell +0.6 %, cornell_glass +1.7 %, cornell_mirror +1.5 %; not for BVH traversal
+    // (complex -4.6 %: its lanes' traversal costs differ more than their path lengths)
+    if (c->streams_req == 0 && S >= 4 && !bvh) S = (S + 1) / 2;
+    c->last_streams = S;
     const int kidx = bvh ? 17 : (a.n <= 16 ? (int)a.n : 0);
     if (bvh) {
         a.bvh_nodes = c->d_bvh_nodes; a.bvh_geom = c->d_bvh_geom; a.bvh_ids = c->d_bvh_ids;

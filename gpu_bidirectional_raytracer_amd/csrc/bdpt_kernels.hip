@@ -275,6 +275,14 @@ __device__ __forceinline__ f3 cosine_tail(f3 w, f3 u, float u_phi, float u_r2, f
 #ifndef BDPT_REGEN_K
 #define BDPT_REGEN_K 48
 #endif
+// The same grouping for pass-stream lanes that render more than one pass (S < npass; the auto
+// stream mode runs two passes per lane, bdpt_host.cpp); then the planar RNG copy is read too (a
+// group restarts on one slot, so one sid and depth).  Two passes per lane with grouping against
+// one pass per lane, one-session A/B (profiles/r03_s16_ab_regen_streams.txt): cornell +0.7 %,
+// cornell_glass +0.8 %, synthetic64 -0.2 %; without grouping two passes per lane cost 3.5-6 %.
+#ifndef BDPT_REGEN_STREAMS
+#define BDPT_REGEN_STREAMS 1
+#endif
 #ifndef BDPT_CAMB
 #define BDPT_CAMB 1
 #endif
@@ -769,7 +777,8 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
 #if BDPT_RAND_PLANAR
     // one pass per lane (pass streams, S = npass): the lanes of a wave stay on one sid and depth,
     // so their gathers are adjacent in the planar copy (wave-uniform choice)
-    const bool planar = STREAMS && nslot == 1 && a.rndp != nullptr;
+    const bool planar = STREAMS && (nslot == 1 || BDPT_REGEN_STREAMS) && a.rndp != nullptr;
+    constexpr bool kRegen = BDPT_REGEN_K > 1 && (!STREAMS || BDPT_REGEN_STREAMS);
     const __amdgpu_buffer_rsrc_t rsp = __builtin_amdgcn_make_buffer_rsrc(
         (void*)a.rndp, (short)0, (int)(BDPT_DEV_RANDP_PLANES * BDPT_DEV_RANDP_PL * 4u), 0x00020000);
     if (planar) load_rand5p(rsp, j, q0, q1, q2, q3, q4);
@@ -1325,7 +1334,7 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                 depth = 0;
                 const int pn = s0 + k * S;
                 alive = pn < a.npass && cnt0 + (unsigned)pn < BDPT_DEV_COUNTER_CAP;
-                if constexpr (!STREAMS && BDPT_REGEN_K > 1) {
+                if constexpr (kRegen) {
                     parked = alive;
                     alive = false;
                 }
@@ -1345,7 +1354,7 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                 load_rand5(rnd, j, q0, q1, q2, q3, q4);
             }
         }
-        if constexpr (!STREAMS && BDPT_REGEN_K > 1) {
+        if constexpr (kRegen) {
             // release the parked lanes together (wave-uniform decision)
             const unsigned long long mp = __builtin_amdgcn_ballot_w64(parked);
             if (mp != 0 && (__popcll(mp) >= BDPT_REGEN_K || __builtin_amdgcn_ballot_w64(alive) == 0)) {
@@ -1355,7 +1364,12 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                     unsigned xyv = xy;
                     asm volatile("" : "+v"(xyv));
                     const unsigned li = (xyv >> 16) * (unsigned)a.W + (xyv & 0xffffu);
-                    load_rand5(rnd, (26u + li * 25u + SID[k]) % M5, q0, q1, q2, q3, q4);
+                    const unsigned jr = (26u + li * 25u + SID[k]) % M5;
+#if BDPT_RAND_PLANAR
+                    if (planar) load_rand5p(rsp, jr, q0, q1, q2, q3, q4);
+                    else
+#endif
+                    load_rand5(rnd, jr, q0, q1, q2, q3, q4);
                 }
             }
         }

@@ -1,9 +1,10 @@
 #!/bin/bash
 # Per-workload profiles on the GPU box: for each bench.py workload, one rocprofv3 kernel-trace
 # --stats run of the default bench command and the PMC passes (separate runs, MI355X_MICROARCH.md
-# "HBM") with the pass-stream mode the default run settles on (-1: one pass per lane, 1: fused);
+# "HBM") with the pass-stream mode the default run settles on (S = half the launch's passes: two
+# passes per lane; 1: fused);
 # the last two passes split the VALU instructions by class (scripts/valu_weighted.py).
-#   WORKLOADS="cornell1080:-1 caustic8:1 weak64:-1" bash scripts/profile_workloads.sh
+#   WORKLOADS="cornell1080:16 caustic8:1 weak64:32" bash scripts/profile_workloads.sh
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out; export TMPDIR=/tmp
@@ -18,7 +19,7 @@ PMC_SETS=(
   "SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 GRBM_GUI_ACTIVE"
   "SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE"
 )
-for ws in ${WORKLOADS:-cornell1080:-1 caustic8:1 weak64:-1}; do
+for ws in ${WORKLOADS:-cornell1080:16 caustic8:1 weak64:32}; do
   w=${ws%%:*}; S=${ws##*:}
   steps=${STEPS_STATS:-10}
   [ "$w" = weak64 ] && steps=${STEPS_STATS64:-6}

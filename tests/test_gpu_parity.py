@@ -204,26 +204,26 @@ def test_per_lane_streams_policy(gpu):
 
 @pytest.mark.parametrize("name", ["cornell", "caustic"])
 def test_auto_streams_measured(gpu, rnd0, name):
-    """Auto (0): the first three calls of >= 2 passes run one pass per lane, the fused kernel
-    and one pass per lane again; later calls use the fused kernel only if it measured faster than
-    both pass-stream calls; a scene change measures again.  Every call's result is the oracle's
-    whatever was chosen."""
+    """Auto (0): the first three calls of >= 2 passes run pass streams (two passes per lane in
+    launches of >= 4 passes), the fused kernel and pass streams again; later calls use the fused
+    kernel only if it measured faster than both pass-stream calls; a scene change measures again.
+    Every call's result is the oracle's whatever was chosen."""
     W, H = 97, 65
     r, cam, sp = make(name, W, H, gpu)
     sid, vlp = schedule(48)
     r.path_passes(sid[:1], vlp[:1])                        # 1 pass: not a measurement
     assert r.last_streams == 1
     r.path_passes(sid[1:9], vlp[1:9])
-    assert r.last_streams == 8                             # measures pass streams
+    assert r.last_streams == 4                             # measures pass streams (2 per lane)
     r.path_passes(sid[9:17], vlp[9:17])
     assert r.last_streams == 1                             # measures the fused kernel
     r.path_passes(sid[17:25], vlp[17:25])
-    assert r.last_streams == 8                             # pass streams again
+    assert r.last_streams == 4                             # pass streams again
     used = []
     for a0 in (25, 33):
         r.path_passes(sid[a0:a0 + 8], vlp[a0:a0 + 8])
         used.append(r.last_streams)
-    assert used[0] == used[1] and used[0] in (1, 8), used
+    assert used[0] == used[1] and used[0] in (1, 4), used
     col, cnt = r.read_radiance()
     lp = oracle.light_pass(sp, rnd0, 0)
     ocol, ocnt, opix = oracle.path_passes(sp, rnd0, cam, W, H, lp, sid[:41], vlp[:41])
@@ -232,7 +232,7 @@ def test_auto_streams_measured(gpu, rnd0, name):
     assert_same(r.read_pixels(), opix, "pixels")
     r.set_scene(sp)                                        # ReInitScene: measure again
     r.path_passes(sid[41:48], vlp[41:48])
-    assert r.last_streams == 7
+    assert r.last_streams == 4                             # 7 passes, two per lane
     r.close()
 
 

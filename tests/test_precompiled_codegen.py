@@ -12,8 +12,8 @@ Recorded values and why they are acceptable:
     N = 11 spheres the SGPR file (106) overflows by 2 per extra sphere and the excess goes to VGPR
     lanes (v_writelane / v_readlane, no memory traffic).  These instances only run with
     specialisation off: by default a <= 64-sphere scene runs its hipRTC build;
-  * the BVH instance keeps its traversal state in SGPRs and moves 6 (fused) / 8 (pass streams) of
-    them to VGPR lanes in the same way.
+  * the BVH instance keeps its traversal state in SGPRs and moves 10 of them to VGPR lanes in the
+    same way (6 / 8 before the grouped path regeneration of round 3).
 """
 import os
 import subprocess
@@ -30,7 +30,7 @@ sys.path.insert(0, os.path.join(REPO, "tools"))
 
 def _sgpr_spills(n, streams):
     if n == -1:
-        return 8 if streams else 6
+        return 10
     return 2 * (n - 10) if n > 10 else 0
 
 
