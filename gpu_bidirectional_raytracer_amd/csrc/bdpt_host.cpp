@@ -89,19 +89,22 @@ struct bdpt_ctx {
     bool rand_ready = false;
     int shard = 0, nshards = 1, band_rows = 8;
     int streams_req = 0;                // bdpt_set_streams: 0 = auto (measured), -1 = one pass per lane
-    // auto mode: the first three calls of >= 2 passes run the pass-stream kernels (one pass per
-    // lane), the fused S = 1 kernel, and the pass-stream kernels again; the fused kernel is kept
-    // only if its device time per pass beats the faster of the two pass-stream calls by
-    // kTuneMargin (a cold first call -- clocks still ramping -- no longer decides for the fused
-    // kernel).  tune_phase 0..2: measuring; 3: all issued; 4: decided.  Reset by scene / shard /
-    // traversal / specialisation / stream-mode changes.  BDPT_STREAMS_TUNE=0: no measurement.
+    // auto mode: the first four calls of >= 2 passes run the pass-stream kernels, the fused S = 1
+    // kernel with paired segment loads (bdpt_kernels.hip BDPT_RNG_PAIR), the pass-stream kernels
+    // again and the fused kernel without pairing; the faster fused variant is kept only if its
+    // device time per pass beats the faster of the two pass-stream calls by kTuneMargin (a cold
+    // first call -- clocks still ramping -- no longer decides for the fused kernel).  tune_phase
+    // 0..3: measuring; 4: all issued; 5: decided.  Reset by scene / shard / traversal /
+    // specialisation / stream-mode changes.  BDPT_STREAMS_TUNE=0: no measurement.
     static constexpr double kTuneMargin = 0.02;
+    static constexpr int kTunePhases = 4;
     bool tune_enabled = true;
     int tune_phase = 0;
     bool tune_fused = false;
-    long long tune_call[3] = {-1, -1, -1};
-    double tune_ms[3] = {0.0, 0.0, 0.0};
-    int tune_npass[3] = {0, 0, 0};
+    bool tune_pair = true;              // the fused variant kept: paired segment loads or not
+    long long tune_call[kTunePhases] = {-1, -1, -1, -1};
+    double tune_ms[kTunePhases] = {0.0, 0.0, 0.0, 0.0};
+    int tune_npass[kTunePhases] = {0, 0, 0, 0};
     int last_streams = 1;               // S of the last path-pass launch
     bool last_bvh = false;              // the last path-pass launch traversed the BVH
     int cus = 256;                      // compute units (auto stream count)
@@ -499,7 +502,7 @@ static int fused_max_passes() {
 
 // The specialised kernel for the context's scene and pass-stream mode, compiled on first use;
 // nullptr = use the precompiled instance (reason in c->jit_err).
-static hipFunction_t jit_path_kernel(bdpt_ctx* c, bool streams) {
+static hipFunction_t jit_path_kernel(bdpt_ctx* c, bool streams, bool pair = true) {
     const unsigned n = (unsigned)c->spheres.size();
     if (!c->specialize || n < 1 || n > 64) return nullptr;          // kJitEmis is 64 bits
     unsigned long long emis = 0;
@@ -554,6 +557,7 @@ static hipFunction_t jit_path_kernel(bdpt_ctx* c, bool streams) {
             "-DBDPT_WAVES_PER_SIMD=" + std::to_string(waves)};
         std::vector<std::string> all = opts;
         if (!streams) all.push_back("-DBDPT_FUSED_WAVES=" + std::to_string(waves));
+        if (!streams && !pair) all.push_back("-DBDPT_RNG_PAIR=0");
         if (const char* extra = getenv("BDPT_JIT_FLAGS")) {    // experiments: extra -D options
             std::string tok;
             for (const char* q = extra;; q++) {
@@ -622,7 +626,7 @@ static int fold_timing(bdpt_ctx* c, long long upto) {
         HIPCHK(c, hipEventElapsedTime(&ms, s.ev0, s.ev1));
         c->last_ms = ms;
         c->acc_ms += ms;
-        for (int r = 0; r < 3; r++)
+        for (int r = 0; r < bdpt_ctx::kTunePhases; r++)
             if (c->folded == c->tune_call[r]) c->tune_ms[r] = ms;
         for (int k = 0; k < s.launches; k++) {
             float km = 0.f;
@@ -1003,19 +1007,24 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
     if (S <= 0) S = BDPT_MAX_STREAMS;
     // auto: measure both kernels on the first two calls, then keep the faster
     int tune_role = -1;
+    bool pair = true;                                        // fused kernel: paired segment loads
     if (c->streams_req == 0 && c->tune_enabled) {
-        if (c->tune_phase == 3) {                            // waits for the last measured call
-            if (int rc = fold_timing(c, c->tune_call[2] + 1)) return rc;
+        if (c->tune_phase == bdpt_ctx::kTunePhases) {        // waits for the last measured call
+            if (int rc = fold_timing(c, c->tune_call[bdpt_ctx::kTunePhases - 1] + 1)) return rc;
             const double a0 = c->tune_ms[0] / c->tune_npass[0], a2 = c->tune_ms[2] / c->tune_npass[2];
-            const double fused = c->tune_ms[1] / c->tune_npass[1];
+            const double fp = c->tune_ms[1] / c->tune_npass[1], fn = c->tune_ms[3] / c->tune_npass[3];
+            c->tune_pair = fp <= fn;
+            const double fused = c->tune_pair ? fp : fn;
             c->tune_fused = fused * (1.0 + bdpt_ctx::kTuneMargin) < (a0 < a2 ? a0 : a2);
-            c->tune_phase = 4;
+            c->tune_phase = bdpt_ctx::kTunePhases + 1;
         }
-        if (c->tune_phase < 3 && npass >= 2) {
+        if (c->tune_phase < bdpt_ctx::kTunePhases && npass >= 2) {
             tune_role = c->tune_phase;
-            if (tune_role == 1) S = 1;
-        } else if (c->tune_phase == 4 && c->tune_fused) {
+            if (tune_role == 1 || tune_role == 3) S = 1;
+            pair = tune_role != 3;
+        } else if (c->tune_phase == bdpt_ctx::kTunePhases + 1 && c->tune_fused) {
             S = 1;
+            pair = c->tune_pair;
         }
     }
     a.nloc = (int)lanes;
@@ -1090,7 +1099,7 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
         any_fused |= !st;
         if (bvh) continue;
         if (st && !jf_streams) jf_streams = jit_path_kernel(c, true);
-        if (!st && !jf_fused) jf_fused = jit_path_kernel(c, false);
+        if (!st && !jf_fused) jf_fused = jit_path_kernel(c, false, pair);
     }
     // a fused launch updates colors itself: it waits for the outstanding fold, before the call's
     // timing starts (so the stream-mode measurement does not charge that fold to it)

@@ -283,6 +283,21 @@ __device__ __forceinline__ f3 cosine_tail(f3 w, f3 u, float u_phi, float u_r2, f
 #ifndef BDPT_REGEN_STREAMS
 #define BDPT_REGEN_STREAMS 1
 #endif
+// Fused kernel: a parking lane loads its next pass's first-segment randoms at once (it waits at
+// least an iteration before it uses them), and its camera randoms a second time into cr0, cr1
+// (buffer loads, so the compiler does not merge them with the q0, q1 loads).  caustic8 +1.9 %,
+// open +0.3 % in one-session A/B (profiles/r03_s19_ab_park_prefetch.txt); pass streams keep
+// loading at release (cornell -1.1 % with it).  An ablation without any table reads runs caustic8
+// 37 % faster: the fused kernel's random gathers (20 B per lane and segment at unrelated
+// addresses, 6.6 TB/s of L2 fills) are what is left to win on open scenes.
+#ifndef BDPT_PARK_PREFETCH
+#define BDPT_PARK_PREFETCH 1
+#endif
+// Fused kernel: the randoms of two segments (depth d even and d + 1) are loaded together, so a
+// path's table line is fetched once for both instead of being evicted from L2 between them
+#ifndef BDPT_RNG_PAIR
+#define BDPT_RNG_PAIR 1
+#endif
 #ifndef BDPT_CAMB
 #define BDPT_CAMB 1
 #endif
@@ -777,14 +792,35 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
 #if BDPT_RAND_PLANAR
     // one pass per lane (pass streams, S = npass): the lanes of a wave stay on one sid and depth,
     // so their gathers are adjacent in the planar copy (wave-uniform choice)
+    // (the fused kernel keeps the linear table: its lanes are on different passes and depths, and
+    // planar reads measured -57 % on caustic8, -38 % with whole-wave lockstep groups)
     const bool planar = STREAMS && (nslot == 1 || BDPT_REGEN_STREAMS) && a.rndp != nullptr;
     constexpr bool kRegen = BDPT_REGEN_K > 1 && (!STREAMS || BDPT_REGEN_STREAMS);
+    constexpr bool kParkPf = kRegen && BDPT_PARK_PREFETCH && !STREAMS;
+    float cr0 = 0.f, cr1 = 0.f;                     // camera randoms of a released lane (kParkPf)
+    // (read through a buffer descriptor: the compiler would otherwise merge them with the q0, q1
+    // loads of the same addresses and copy them over behind a vmcnt(0))
+    const __amdgpu_buffer_rsrc_t rsl = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)rnd, (short)0, (int)(kRandN * 4u), 0x00020000);
+    auto load_cam = [&](unsigned jc) {
+        cr0 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsl, jc * 4u, 0, 0));
+        cr1 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsl, jc * 4u, 4, 0));
+    };
     const __amdgpu_buffer_rsrc_t rsp = __builtin_amdgcn_make_buffer_rsrc(
         (void*)a.rndp, (short)0, (int)(BDPT_DEV_RANDP_PLANES * BDPT_DEV_RANDP_PL * 4u), 0x00020000);
     if (planar) load_rand5p(rsp, j, q0, q1, q2, q3, q4);
     else
 #endif
     load_rand5(rnd, j, q0, q1, q2, q3, q4);
+    // BDPT_RNG_PAIR: n0..n4 = the next segment's randoms, loaded with q0..q4 at even depths
+    constexpr bool kPair = !STREAMS && BDPT_RNG_PAIR;
+    float n0 = 0.f, n1 = 0.f, n2 = 0.f, n3 = 0.f, n4 = 0.f;
+    auto load_next = [&](unsigned jj) {                 // segment depth + 1: (jj + 5) mod (RAND_N - 5)
+        const unsigned jn = jj + 5u < M5 ? jj + 5u : jj + 5u - M5;
+        load_rand5(rnd, jn, n0, n1, n2, n3, n4);
+    };
+    if constexpr (kPair) load_next(j);
+    if constexpr (kParkPf) load_cam(j);
     f3 ro = mk(0.f, 0.f, 0.f), rd = ro, thr = ro, rad = ro, nl = ro;
     bool specular = true, fresh = true, parked = false;
     bool alive = active && nslot > 0 && cnt0 + (unsigned)s0 < BDPT_DEV_COUNTER_CAP;
@@ -808,8 +844,9 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
 #if BDPT_CAMB
                 // device.cu:565-566: ((float)x*iw - iw*W/2.) + d_Rand[kk]*iw in fp64, then fp32
                 const double2 cb = camb[threadIdx.x];
-                const float kx = (float)(cb.x + (double)(q0 * k4.x));
-                const float ky = (float)(cb.y + (double)(q1 * k4.y));
+                const float u0 = kParkPf ? cr0 : q0, u1 = kParkPf ? cr1 : q1;
+                const float kx = (float)(cb.x + (double)(u0 * k4.x));
+                const float ky = (float)(cb.y + (double)(u1 * k4.y));
                 f3 rdir = mk(0.f, 0.f, 0.f);
                 rdir = add(rdir, smul(kx, mk(c0.x, c0.y, c0.z)));
                 rdir = add(rdir, smul(ky, mk(c1.x, c1.y, c1.z)));
@@ -1339,10 +1376,13 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                     alive = false;
                 }
             }
-            if (alive) {                  // prefetch the next segment's random numbers (:619)
+            if (alive || (kParkPf && parked)) {   // prefetch the next segment's randoms (:619)
                 // 26 + 25 i and the pass's sid are rebuilt here rather than kept live across the
                 // loop (one LDS read and four integer ops per segment, against a spill; keeping j
                 // live and adding 5 per segment measured 1 % slower)
+                if (kPair && (depth & 1u)) {             // loaded with the previous segment's
+                    q0 = n0; q1 = n1; q2 = n2; q3 = n3; q4 = n4;
+                } else {
                 unsigned xyv = xy;
                 asm volatile("" : "+v"(xyv));
                 const unsigned li = (xyv >> 16) * (unsigned)a.W + (xyv & 0xffffu);
@@ -1352,6 +1392,9 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                 else
 #endif
                 load_rand5(rnd, j, q0, q1, q2, q3, q4);
+                if (kPair) load_next(j);
+                if (kParkPf && parked) load_cam(j);
+                }
             }
         }
         if constexpr (kRegen) {
@@ -1361,6 +1404,8 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                 if (parked) {
                     parked = false;
                     alive = true;
+                }
+                if (!kParkPf && alive && fresh) {        // without BDPT_PARK_PREFETCH: load now
                     unsigned xyv = xy;
                     asm volatile("" : "+v"(xyv));
                     const unsigned li = (xyv >> 16) * (unsigned)a.W + (xyv & 0xffffu);
