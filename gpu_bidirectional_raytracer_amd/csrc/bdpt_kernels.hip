@@ -1415,6 +1415,7 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                     else
 #endif
                     load_rand5(rnd, jr, q0, q1, q2, q3, q4);
+                    if (kPair) load_next(jr);
                 }
             }
         }
