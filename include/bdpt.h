@@ -101,7 +101,7 @@ int  bdpt_set_shard(bdpt_ctx *ctx, int shard, int nshards, int band_rows);
  *        pass per lane; two per lane, S = ceil(passes / 2), in launches of >= 4 passes that do
  *        not use the BVH), the fused kernel with paired segment loads, the pass-stream kernel
  *        again and the fused kernel without pairing; later calls use the faster fused variant
- *        only if its device time per pass beat both pass-stream calls by 2 % (closed scenes with
+ *        only if its device time per pass beat both pass-stream calls by 5 % (closed scenes with
  *        long paths favour pass streams, open scenes with short paths the fused kernel);
  *        re-measured after a scene / shard / traversal change;
  *  -1  = BDPT_STREAMS_PER_LANE: always one pass per lane (S = passes per launch, <= 128);
