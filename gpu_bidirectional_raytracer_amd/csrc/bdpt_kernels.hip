@@ -265,7 +265,6 @@ __device__ __forceinline__ f3 cosine_tail(f3 w, f3 u, float u_phi, float u_r2, f
 #ifndef BDPT_PACK_EDGES
 #define BDPT_PACK_EDGES 1
 #endif
-// camera terms: per-lane fp64 base in LDS, kz products formed once per workgroup
 // Fused S = 1 kernel: a lane whose path ends parks until at least BDPT_REGEN_K lanes of its wave
 // (or all of its live lanes) are parked; then they start their next passes together, so the
 // camera-ray and path-start code runs for groups of lanes instead of a few lanes in almost every
@@ -295,9 +294,12 @@ __device__ __forceinline__ f3 cosine_tail(f3 w, f3 u, float u_phi, float u_r2, f
 #endif
 // Fused kernel: the randoms of two segments (depth d even and d + 1) are loaded together, so a
 // path's table line is fetched once for both instead of being evicted from L2 between them
+// (caustic8 +9 %, open -4 %: the auto stream mode measures the fused kernel with and without it
+// and keeps the faster, bdpt_host.cpp; profiles/r03_s22_ab_rng_pair.txt)
 #ifndef BDPT_RNG_PAIR
 #define BDPT_RNG_PAIR 1
 #endif
+// camera terms: per-lane fp64 base in LDS, kz products formed once per workgroup
 #ifndef BDPT_CAMB
 #define BDPT_CAMB 1
 #endif
