@@ -1,11 +1,13 @@
-"""Single-GPU rehearsal of the multi-GPU weak-scaling step (bench.py --gpus N).
+"""Single-GPU rehearsal of the multi-GPU step (bench.py --gpus N).
 
-For each N, rank 0's share of an N-way band shard (1/N of the rows, N x passes) is rendered on
-one GPU with auto pass streams and with S = 1, and its device time is compared with the N = 1
-step; efficiency = t(N=1) / t(rank share).  The RCCL reduce is not included (it runs once per
-frame, not per step).
+For each N, the first and last rank's share of an N-way band shard (1/N of the rows; N x passes
+for weak scaling, the same passes with --strong) is rendered on one GPU with auto pass streams
+(after the auto mode's four measured calls) and with the S values asked for, and its device time
+is compared with the N = 1 step: efficiency = t(N=1) / t(rank share), over N for --strong.  The
+RCCL reduce is not included (it runs once per frame, not per step).
 
     python scripts/shard_probe.py [--scene cornell] [--passes 16] [--reps 3]
+    python scripts/shard_probe.py --scene caustic --passes 128 --strong --streams 1,32
 """
 import argparse
 import json
@@ -18,16 +20,20 @@ sys.path.insert(0, REPO)
 import gpu_bidirectional_raytracer_amd as g  # noqa: E402
 
 
+WARM = 5
+
+
 def run(sp, cam, W, H, sid, vlp, shard, nshards, band, streams, reps):
     r = g.Renderer(sp, W, H, cam, device=0)
     r.set_shard(shard, nshards, band)
     r.set_streams(streams)
     r.light_pass(0)
-    n = len(sid) // (reps + 1)
-    r.path_passes(sid[:n], vlp[:n])                     # warmup
+    n = len(sid) // (reps + WARM)
+    for k in range(WARM):                               # warm-up (the auto mode measures 4 calls)
+        r.path_passes(sid[k * n:(k + 1) * n], vlp[k * n:(k + 1) * n])
     r.synchronize()
     r.path_timing(reset=True)
-    for k in range(1, reps + 1):
+    for k in range(WARM, WARM + reps):
         r.path_passes(sid[k * n:(k + 1) * n], vlp[k * n:(k + 1) * n])
     r.synchronize()
     ms, launches = r.path_timing()
@@ -44,6 +50,7 @@ def main():
     ap.add_argument("--band-rows", type=int, default=8)
     ap.add_argument("--ns", default="1,2,4,8")
     ap.add_argument("--streams", default="", help="S values to try besides auto, e.g. 1,2,8")
+    ap.add_argument("--strong", action="store_true", help="same passes for every N (strong scaling)")
     args = ap.parse_args()
     W, H = 1921, 1081
     cam, sp = g.read_scene(os.path.join(REPO, "assets", "scenes", args.scene + ".scn"))
@@ -52,18 +59,20 @@ def main():
     sched.light()
     t1 = None
     for N in [int(x) for x in args.ns.split(",")]:
-        sid, vlp = sched.next(args.passes * N * (args.reps + 1))
+        per = args.passes * (1 if args.strong else N)
+        sid, vlp = sched.next(per * (args.reps + WARM))
         extra = [int(x) for x in args.streams.split(",") if x] if args.streams else ([] if N == 1 else [1])
         for streams in [0] + extra:
             worst = 0.0
             for shard in sorted({0, N - 1}):
                 ms, S = run(sp, cam, W, H, sid, vlp, shard, N, args.band_rows, streams, args.reps)
                 worst = max(worst, ms)
-            if N == 1:
+            if N == 1 and streams == 0:
                 t1 = worst
+            eff = t1 / worst / (N if args.strong else 1)
             print(json.dumps({"N": N, "streams_req": streams, "streams": S, "ms_per_step": round(worst, 3),
-                              "efficiency": round(t1 / worst, 4),
-                              "whole_job_Msamples_s": round(W * H * args.passes * N / worst / 1e3, 1)}),
+                              "efficiency": round(eff, 4),
+                              "whole_job_Msamples_s": round(W * H * per / worst / 1e3, 1)}),
                   flush=True)
 
 
