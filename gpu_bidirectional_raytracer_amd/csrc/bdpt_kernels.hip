@@ -206,9 +206,11 @@ __device__ __forceinline__ troots roots_of(tdet q) {
 // key otherwise: the closest-hit update becomes one min3 with the running key (plus the compare
 // and select of the index), and the shadow test one unsigned compare against key(maxt) (0 when
 // maxt <= EPS or NaN: nothing occludes, as in the float test).
-// On in the scene-specialised kernels: cornell +0.7 to +1.1 %, cornell_glass +0.6 %, synthetic64
-// +-0.1 % (one session, profiles/r03_s33_ab_ikey.txt); with the min3 written in C the compiler
-// emits two v_min_u32 and the kernels run 0.5-1 % slower than without keys.
+// (The rule is checked on edge values and random roots by tests/test_ikey_rule.py.)  On in the
+// scene-specialised kernels: cornell +0.7 to +1.1 %, cornell_glass +0.6 %, synthetic64 +-0.1 %,
+// fused caustic / open +0.4 to +1.5 %, simple +3 to +4 % (one session each,
+// profiles/r03_s33_ab_ikey.txt); with the min3 written in C the compiler emits two v_min_u32
+// and the kernels run 0.5-1 % slower than without keys.
 #ifndef BDPT_IKEY
 #ifdef BDPT_JIT
 #define BDPT_IKEY 1
