@@ -34,3 +34,22 @@ def test_cpu_backend_random_scene(rnd0, seed):
     assert np.array_equal(cnt, ocnt)
     assert np.array_equal(col.view(np.uint32), ocol.view(np.uint32)), f"seed {seed}"
     assert np.array_equal(px, opx)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_cpu_backend_random_large_scene(rnd0, seed):
+    from test_gpu_fuzz import random_large_scene
+    cam, sp = random_large_scene(2000 + seed)
+    g.update_camera(cam, W, H)
+    r = g.Renderer(sp, W, H, cam, device=-1)                # BDPT_DEVICE_CPU
+    r.light_pass(0)
+    s = g.PassScheduler()
+    s.light()
+    sid, vlp = s.next(3)
+    r.path_passes(sid, vlp)
+    col, cnt = r.read_radiance()
+    r.close()
+    lp = oracle.light_pass(sp, rnd0, 0)
+    ocol, ocnt, _ = oracle.path_passes(sp, rnd0, cam, W, H, lp, sid, vlp)
+    assert np.array_equal(cnt, ocnt)
+    assert np.array_equal(col.view(np.uint32), ocol.view(np.uint32)), f"seed {seed}"

@@ -83,3 +83,46 @@ def test_random_scene_bit_exact(gpu, rnd0, seed, streams):
     bad = int((col.view(np.uint32) != ocol.view(np.uint32)).sum())
     assert bad == 0, f"seed {seed} streams {streams}: {bad} colour values differ ({len(sp)} spheres)"
     assert np.array_equal(px, opx)
+
+
+def random_large_scene(seed):
+    """Cornell-like wall box (or none) with 150-400 small spheres: the BVH path (bdpt_bvh.cpp,
+    kernel instance N = -1) and the generic every-sphere loop."""
+    rng = np.random.default_rng(seed)
+    cam, sp = random_scene(seed)
+    walls = sp[sp["rad"] >= 1e3]
+    n = int(rng.integers(150, 401))
+    extra = np.zeros(n, g.SPHERE_DTYPE)
+    extra["rad"] = np.exp(rng.uniform(np.log(0.3), np.log(6.0), n)).astype(np.float32)
+    extra["p"] = (rng.uniform(0, 1, (n, 3)) * np.array([100.0, 80.0, 170.0])).astype(np.float32)
+    extra["c"] = rng.uniform(0, 1, (n, 3)).astype(np.float32)
+    extra["c"][rng.random(n) < 0.1] = 0
+    extra["refl"] = rng.choice(4, n, p=[0.6, 0.15, 0.15, 0.1])
+    lit = rng.permutation(n)[:int(rng.integers(1, 4))]
+    extra["e"][lit] = rng.uniform(1, 30, (len(lit), 3)).astype(np.float32)
+    return cam, np.concatenate([walls, extra])
+
+
+@pytest.mark.parametrize("traversal", ["bvh", "brute"])
+@pytest.mark.parametrize("seed", range(6))
+def test_random_large_scene_bit_exact(gpu, rnd0, seed, traversal):
+    cam, sp = random_large_scene(2000 + seed)
+    g.update_camera(cam, W, H)
+    r = g.Renderer(sp, W, H, cam, device=gpu)
+    r.set_traversal(traversal)
+    r.light_pass(0)
+    s = g.PassScheduler()
+    s.light()
+    sid, vlp = s.next(4)
+    r.path_passes(sid, vlp)
+    col, cnt = r.read_radiance()
+    px = r.read_pixels()
+    has_bvh = r.has_bvh
+    r.close()
+    lp = oracle.light_pass(sp, rnd0, 0)
+    ocol, ocnt, opx = oracle.path_passes(sp, rnd0, cam, W, H, lp, sid, vlp)
+    assert has_bvh
+    assert np.array_equal(cnt, ocnt)
+    bad = int((col.view(np.uint32) != ocol.view(np.uint32)).sum())
+    assert bad == 0, f"seed {seed} {traversal}: {bad} colour values differ ({len(sp)} spheres)"
+    assert np.array_equal(px, opx)
