@@ -126,3 +126,33 @@ def test_random_large_scene_bit_exact(gpu, rnd0, seed, traversal):
     bad = int((col.view(np.uint32) != ocol.view(np.uint32)).sum())
     assert bad == 0, f"seed {seed} {traversal}: {bad} colour values differ ({len(sp)} spheres)"
     assert np.array_equal(px, opx)
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_random_call_sequence_bit_exact(gpu, rnd0, seed):
+    """A random scene and frame size rendered by a random sequence of calls (1-40 passes each) in
+    the auto stream mode, which measures pass streams and both fused variants on its first calls
+    and then keeps one: passes rendered by different kernel kinds accumulate into one frame, which
+    must equal the oracle's after every call."""
+    rng = np.random.default_rng(3000 + seed)
+    cam, sp = random_scene(3000 + seed)
+    w, h = int(rng.integers(1, 80)), int(rng.integers(1, 50))
+    g.update_camera(cam, w, h)
+    r = g.Renderer(sp, w, h, cam, device=gpu)
+    r.light_pass(0)
+    r.set_streams(0)
+    lp = oracle.light_pass(sp, rnd0, 0)
+    s = g.PassScheduler()
+    s.light()
+    ocol = ocnt = None
+    for call in range(7):
+        n = int(rng.integers(1, 41))
+        sid, vlp = s.next(n)
+        r.path_passes(sid, vlp)
+        ocol, ocnt, opx = oracle.path_passes(sp, rnd0, cam, w, h, lp, sid, vlp, colors=ocol, counter=ocnt)
+        col, cnt = r.read_radiance()
+        assert np.array_equal(cnt, ocnt), f"seed {seed} call {call}"
+        bad = int((col.view(np.uint32) != ocol.view(np.uint32)).sum())
+        assert bad == 0, f"seed {seed} call {call} ({n} passes, {w}x{h}, S={r.last_streams}): {bad} differ"
+        assert np.array_equal(r.read_pixels(), opx)
+    r.close()
