@@ -156,3 +156,36 @@ def test_random_call_sequence_bit_exact(gpu, rnd0, seed):
         assert bad == 0, f"seed {seed} call {call} ({n} passes, {w}x{h}, S={r.last_streams}): {bad} differ"
         assert np.array_equal(r.read_pixels(), opx)
     r.close()
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_shards_sum_to_oracle(gpu, rnd0, seed):
+    """A random scene cut into 2-8 interleaved bands of 1-24 rows (bdpt_set_shard), each band set
+    rendered by its own context in the auto stream mode: every pixel is rendered by exactly one
+    shard, and the sum of the shards is the oracle's frame bit for bit."""
+    rng = np.random.default_rng(4000 + seed)
+    cam, sp = random_scene(4000 + seed)
+    w, h = int(rng.integers(8, 70)), int(rng.integers(8, 60))
+    nsh, band = int(rng.integers(2, 9)), int(rng.choice([1, 3, 8, 16, 24]))
+    g.update_camera(cam, w, h)
+    s = g.PassScheduler()
+    s.light()
+    sid, vlp = s.next(int(rng.integers(2, 12)))
+    acc_c = np.zeros((h, w, 3), np.float32)
+    acc_n = np.zeros((h, w), np.uint32)
+    for k in range(nsh):
+        r = g.Renderer(sp, w, h, cam, device=gpu)
+        r.set_shard(k, nsh, band)
+        r.light_pass(0)
+        r.path_passes(sid, vlp)
+        c, n = r.read_radiance()
+        r.close()
+        owned = (np.arange(h) // band) % nsh == k
+        assert (n[~owned] == 0).all() and (n[owned] == len(sid)).all()
+        acc_c += c
+        acc_n += n
+    lp = oracle.light_pass(sp, rnd0, 0)
+    ocol, ocnt, _ = oracle.path_passes(sp, rnd0, cam, w, h, lp, sid, vlp)
+    assert np.array_equal(acc_n, ocnt)
+    bad = int((acc_c.view(np.uint32) != ocol.view(np.uint32)).sum())
+    assert bad == 0, f"seed {seed} ({nsh} shards of {band} rows, {w}x{h}): {bad} differ"
