@@ -142,6 +142,15 @@ struct bdpt_ctx {
     char jit_err[256] = {0};            // why the last specialisation fell back (diagnostics)
     int jit_waves = 0;                  // waves/SIMD bound of the last specialised build
     bool jit_zero_exit = false;         // the last specialised build has the black-surface exit
+    // jit_path_kernel's answer per [pass streams][paired loads] for the current scene, specialise
+    // switch and BDPT_JIT_FLAGS: a call then resolves its kernel without rebuilding the option
+    // strings (tens of microseconds per call, which the one-pass-per-call pattern pays every call)
+    struct jit_memo_t {
+        bool valid = false, zero_exit = false;
+        hipFunction_t fn = nullptr;
+        int waves = 0;
+        std::string flags, err;
+    } jit_memo[2][2];
     int last_features = 0;              // BDPT_FEAT_* of the last path-pass launch
     unsigned rand_seed = 0;             // seed of the current MT607 table (rand_ready)
     char err[512] = {0};
@@ -181,6 +190,8 @@ static int fail(bdpt_ctx* c, int code, const char* fmt, ...) {
 
 static int upload_scene(bdpt_ctx* c) {
     c->tune_phase = 0;                                      // re-measure the stream mode
+    for (auto& row : c->jit_memo)                           // the specialised kernels change too
+        for (auto& m : row) m.valid = false;
     const unsigned n = (unsigned)c->spheres.size();
     // queued path passes may still read the scene buffers freed / rewritten below
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -504,7 +515,7 @@ static int fused_max_passes() {
 
 // The specialised kernel for the context's scene and pass-stream mode, compiled on first use;
 // nullptr = use the precompiled instance (reason in c->jit_err).
-static hipFunction_t jit_path_kernel(bdpt_ctx* c, bool streams, bool pair = true) {
+static hipFunction_t jit_path_kernel_build(bdpt_ctx* c, bool streams, bool pair) {
     const unsigned n = (unsigned)c->spheres.size();
     if (!c->specialize || n < 1 || n > 64) return nullptr;          // kJitEmis is 64 bits
     unsigned long long emis = 0;
@@ -605,6 +616,29 @@ static hipFunction_t jit_path_kernel(bdpt_ctx* c, bool streams, bool pair = true
             return fn;
         }
     }
+}
+
+static void jit_forget(bdpt_ctx* c) {                   // the scene or the specialise switch changed
+    for (auto& row : c->jit_memo)
+        for (auto& m : row) m.valid = false;
+}
+
+static hipFunction_t jit_path_kernel(bdpt_ctx* c, bool streams, bool pair = true) {
+    const char* jfl = getenv("BDPT_JIT_FLAGS");
+    bdpt_ctx::jit_memo_t& m = c->jit_memo[streams][pair];
+    if (m.valid && strcmp(m.flags.c_str(), jfl ? jfl : "") == 0) {
+        snprintf(c->jit_err, sizeof c->jit_err, "%s", m.err.c_str());
+        if (m.fn) { c->jit_waves = m.waves; c->jit_zero_exit = m.zero_exit; }
+        return m.fn;
+    }
+    hipFunction_t fn = jit_path_kernel_build(c, streams, pair);
+    m.valid = true;
+    m.fn = fn;
+    m.waves = c->jit_waves;
+    m.zero_exit = c->jit_zero_exit;
+    m.flags = jfl ? jfl : "";
+    m.err = c->jit_err;
+    return fn;
 }
 
 // Make the context's stream wait for the last pass-stream fold (issued on fstream): call before
@@ -820,6 +854,7 @@ int bdpt_last_streams(const bdpt_ctx* c) { return c ? c->last_streams : BDPT_EIN
 static int one_set_specialize(bdpt_ctx* c, int on) {
     if (!c) return BDPT_EINVAL;
     c->specialize = on != 0;
+    jit_forget(c);
     c->tune_phase = 0;
     return BDPT_OK;
 }
