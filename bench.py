@@ -28,9 +28,10 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 METRIC = "Msamples/sec (rays·bounces/s) at 1080p cornell.scn, 1/2/4/8 GPU"
+COUNTER_CAP = 30000              # per-pixel pass cap of the path kernel (device.cu:607)
 
 WORKLOADS = {
-    "cornell1080": dict(scene="cornell", width=1920, height=1080, passes=32, band_rows=8, fixed_bands=0,
+    "cornell1080": dict(scene="cornell", width=1920, height=1080, passes=128, band_rows=8, fixed_bands=0,
                         scaling="weak", config="configs[1] scene at 1080p (the metric's config)"),
     "caustic8": dict(scene="caustic", width=1920, height=1080, passes=128, band_rows=8, fixed_bands=0,
                      scaling="strong", config="configs[3]: caustic.scn 1920x1080, pixel bands over N GPUs"),
@@ -400,9 +401,22 @@ def main():
     job_pixels = sum(shd.owned_pixels(W, H, q, nshards, band) for q in range(units))
     own_pixels = shd.owned_pixels(W, H, rank, nshards, band)  # this rank's (or device 0's) share
 
+    # The reference renders pass p of a pixel only while its counter is below 30000
+    # (device.cu:607): a step that crossed it would skip work.  So the accumulation is reset
+    # (bdpt_reset_accum, the reference's ReInit) before a step that would cross it, and every
+    # step, timed or not, renders all of its passes (an async counter memset, inside the clock).
+    if per_step > COUNTER_CAP:
+        raise SystemExit(f"bench.py: {per_step} passes per step exceed the {COUNTER_CAP}-pass counter cap")
+    held = [0, 0]                                             # [passes since the last reset, resets]
+
     def step(k):
+        if held[0] + per_step > COUNTER_CAP:
+            r.reset_accum()
+            held[0] = 0
+            held[1] += 1
         a, b = k * per_step, (k + 1) * per_step
         r.path_passes(sid[a:b], vlp[a:b], sync=False)
+        held[0] += per_step
 
     def barrier():
         if dist is not None:
@@ -457,15 +471,16 @@ def main():
         idents = [gpu_identity(d) for d in devices]
 
     if rank == 0:
-        spp_total = per_step * (untimed + args.steps)
-        if dist is not None or mode == "inproc":              # check the assembled frame's counters
-            if dist is not None:
-                r.update_pixels()
-                cnt = t_cnt.cpu().numpy().reshape(H, W)
-            else:
-                cnt = r.read_radiance()[1]
-            owned = (torch.arange(H).numpy() // band) % nshards < units
-            assert (cnt[owned] == spp_total).all() and (cnt[~owned] == 0).all(), "assembled counters wrong"
+        spp_total = held[0]                                   # passes since the last reset
+        # check the (assembled) frame's counters: every rendered pixel holds every pass since the
+        # last reset, the rest none
+        if dist is not None:
+            r.update_pixels()
+            cnt = t_cnt.cpu().numpy().reshape(H, W)
+        else:
+            cnt = r.read_radiance()[1]
+        owned = (torch.arange(H).numpy() // band) % nshards < units
+        assert (cnt[owned] == spp_total).all() and (cnt[~owned] == 0).all(), "frame counters wrong"
         w = WORK.get(wl["scene"])
         avg_launch_s = kern_ms / 1e3 / max(launches, 1)
         passes_per_launch = per_step * args.steps / max(launches, 1)
@@ -547,7 +562,7 @@ def main():
                                    f"per diffuse vertex; {wl['config']}",
                        "scene": wl["scene"], "width": W, "height": H, "passes_per_step": per_step,
                        "samples_per_step": job_pixels * per_step,
-                       "spp_total": spp_total,
+                       "spp_total": spp_total, "accum_resets": held[1],
                        "parallelism": (f"{nshards} fixed {band}-row bands, GPU r renders band r" if wl["fixed_bands"]
                                        else f"pixel bands x{units} ({band}-row, interleaved)"),
                        "launch": {"single": "one process, one GPU", "ranks": f"torchrun: {world} ranks, one GPU each",

@@ -4,7 +4,7 @@
 # "HBM") with the pass-stream mode the default run settles on (S = half the launch's passes: two
 # passes per lane; 1: fused);
 # the last two passes split the VALU instructions by class (scripts/valu_weighted.py).
-#   WORKLOADS="cornell1080:16 caustic8:1 weak64:32" bash scripts/profile_workloads.sh
+#   WORKLOADS="cornell1080:64 caustic8:1 weak64:32" bash scripts/profile_workloads.sh
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out; export TMPDIR=/tmp
@@ -19,7 +19,7 @@ PMC_SETS=(
   "SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 GRBM_GUI_ACTIVE"
   "SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE"
 )
-for ws in ${WORKLOADS:-cornell1080:16 caustic8:1 weak64:32}; do
+for ws in ${WORKLOADS:-cornell1080:64 caustic8:1 weak64:32}; do
   w=${ws%%:*}; S=${ws##*:}
   steps=${STEPS_STATS:-10}
   [ "$w" = weak64 ] && steps=${STEPS_STATS64:-6}

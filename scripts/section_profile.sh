@@ -9,7 +9,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 out=gpurun_out/section_profile.txt; : > "$out"
-for spec in ${RUNS:-"cornell1080:16" "cornell1080:1" "weak64:32" "caustic8:1"}; do
+for spec in ${RUNS:-"cornell1080:64" "cornell1080:1" "weak64:32" "caustic8:1"}; do
     wl=${spec%%:*}; st=${spec##*:}
     echo "== $wl streams=$st" >> "$out"
     BDPT_PROF=1 BDPT_JIT_FLAGS="-DBDPT_PROF=1 ${EXTRA_FLAGS:-}" timeout -k 10 300 python bench.py --workload "$wl" \
