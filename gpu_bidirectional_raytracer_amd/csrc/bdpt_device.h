@@ -22,6 +22,7 @@
 #define BDPT_DEV_N_PER_RNG 1876
 #define BDPT_DEV_LIGHT_POINTS 4096
 #define BDPT_DEV_COUNTER_CAP 30000u
+#define BDPT_DEV_INLINE_PASSES 16       // launches of <= this many passes carry sid/vlp by value
 #define BDPT_DEV_BVH_EMISSIVE (1 << 30)   // BVH sphere id flag (bdpt_bvh.h kBvhEmissive)
 #define BDPT_DEV_DIFF 0
 #define BDPT_DEV_SPEC 1
@@ -61,9 +62,13 @@ struct bdpt_path_args {
     const float* rnd;
     const float* rndp;              // the planar copy (BDPT_DEV_RANDP_*), pass-stream kernels
     const bdpt_dev_lightpath* lp;
-    const unsigned* sid;            // per pass
+    const unsigned* sid;            // per pass (nullptr: the pass table is sid_inl / vlp_inl)
     const int* vlp;                 // per pass
     int npass;
+    // a launch of <= BDPT_DEV_INLINE_PASSES passes (the reference's one pass per call) carries its
+    // pass table in the arguments: no upload, no copy kernel before the path kernel
+    unsigned sid_inl[BDPT_DEV_INLINE_PASSES];
+    int vlp_inl[BDPT_DEV_INLINE_PASSES];
     bdpt_dev_vec* colors;
     unsigned* counter;
     uchar4* pixels;

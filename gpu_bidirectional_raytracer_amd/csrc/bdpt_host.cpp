@@ -970,9 +970,13 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
     }
     unsigned* hs = c->h_pass + (size_t)slot * 2 * c->pass_cap;
     unsigned* ds = c->d_pass + (size_t)slot * 2 * c->pass_cap;
-    memcpy(hs, sid, sizeof(unsigned) * npass);
-    memcpy(hs + npass, vlp, sizeof(int) * npass);
-    HIPCHK(c, hipMemcpyAsync(ds, hs, sizeof(unsigned) * 2 * npass, hipMemcpyHostToDevice, c->stream));
+    // short calls (the reference's one pass per call) pass their table in the kernel arguments
+    const bool inl = npass <= BDPT_DEV_INLINE_PASSES;
+    if (!inl) {
+        memcpy(hs, sid, sizeof(unsigned) * npass);
+        memcpy(hs + npass, vlp, sizeof(int) * npass);
+        HIPCHK(c, hipMemcpyAsync(ds, hs, sizeof(unsigned) * 2 * npass, hipMemcpyHostToDevice, c->stream));
+    }
     const unsigned* d_sid = ds;
     const int* d_vlp = (const int*)(ds + npass);
     bdpt_ctx::call_slot& cs = c->ring[slot];
@@ -1145,9 +1149,18 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
     HIPCHK(c, hipEventRecord(cs.ev0, c->stream));
     int launches = 0;
     for (int p0 = 0; grid_rows > 0 && p0 < npass; p0 += chunk, launches++) {
-        a.sid = d_sid + p0;
-        a.vlp = d_vlp + p0;
         a.npass = npass - p0 < chunk ? npass - p0 : chunk;
+        if (inl) {
+            a.sid = nullptr;
+            a.vlp = nullptr;
+            for (int q = 0; q < a.npass; q++) {
+                a.sid_inl[q] = sid[p0 + q];
+                a.vlp_inl[q] = vlp[p0 + q];
+            }
+        } else {
+            a.sid = d_sid + p0;
+            a.vlp = d_vlp + p0;
+        }
         // scene tables (4 per sphere, or the BVH: 2 per node + 1 per sphere) + per-pass VLPs +
         // camera + 4 wave shadow queues (results written over maxt) + sids (+ BVH sphere ids)
 #ifdef BDPT_BVH_LDS

@@ -698,11 +698,13 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
     }
     for (int q = threadIdx.x; q < nslot; q += 256) {
         const int pq = s0 + q * S;
-        const bdpt_dev_lightpath L = a.lp[a.vlp[pq] & (BDPT_DEV_LIGHT_POINTS - 1)];
+        const bool inl = a.sid == nullptr;                                // uniform
+        const int vq = inl ? a.vlp_inl[pq & (BDPT_DEV_INLINE_PASSES - 1)] : a.vlp[pq];
+        const bdpt_dev_lightpath L = a.lp[vq & (BDPT_DEV_LIGHT_POINTS - 1)];
         V[3 * q + 0] = make_float4(L.hx, L.hy, L.hz, L.rx);
         V[3 * q + 1] = make_float4(L.ry, L.rz, L.nx, L.ny);
         V[3 * q + 2] = make_float4(L.nz, 0.f, 0.f, 0.f);
-        SID[q] = a.sid[pq];
+        SID[q] = inl ? a.sid_inl[pq & (BDPT_DEV_INLINE_PASSES - 1)] : a.sid[pq];
     }
     if (threadIdx.x == 0) {
         K[0] = make_float4(a.ux[0], a.ux[1], a.ux[2], a.tx);
