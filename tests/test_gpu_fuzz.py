@@ -5,6 +5,8 @@ vary what the specialised kernels' exact shortcuts depend on: wall boxes of radi
 proof (bdpt_host.cpp jit_path_kernel), zero to three emitters, every material (DIFF, SPEC, REFR,
 the LITE tag), spheres that overlap or contain the camera, and cameras inside and outside the
 box.  Reference: device.cu:80-154 (sphere tests), :457-542 (NEE + VLP), :544-791 (path)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -14,6 +16,8 @@ import oracle
 pytestmark = pytest.mark.gpu
 
 W, H, NPASS = 45, 31, 6
+# seeds per test (BDPT_FUZZ_SEEDS=400 for a longer one-off sweep; the suite keeps 40)
+SEEDS = int(os.environ.get("BDPT_FUZZ_SEEDS", "40"))
 
 
 @pytest.fixture(scope="module")
@@ -61,7 +65,7 @@ def random_scene(seed):
 
 
 @pytest.mark.parametrize("streams", [0, 1])
-@pytest.mark.parametrize("seed", range(40))
+@pytest.mark.parametrize("seed", range(SEEDS))
 def test_random_scene_bit_exact(gpu, rnd0, seed, streams):
     cam, sp = random_scene(1000 + seed)
     g.update_camera(cam, W, H)
@@ -104,7 +108,7 @@ def random_large_scene(seed):
 
 
 @pytest.mark.parametrize("traversal", ["bvh", "brute"])
-@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("seed", range(max(6, SEEDS // 8)))
 def test_random_large_scene_bit_exact(gpu, rnd0, seed, traversal):
     cam, sp = random_large_scene(2000 + seed)
     g.update_camera(cam, W, H)
@@ -128,7 +132,7 @@ def test_random_large_scene_bit_exact(gpu, rnd0, seed, traversal):
     assert np.array_equal(px, opx)
 
 
-@pytest.mark.parametrize("seed", range(8))
+@pytest.mark.parametrize("seed", range(max(8, SEEDS // 5)))
 def test_random_call_sequence_bit_exact(gpu, rnd0, seed):
     """A random scene and frame size rendered by a random sequence of calls (1-40 passes each) in
     the auto stream mode, which measures pass streams and both fused variants on its first calls
@@ -158,7 +162,7 @@ def test_random_call_sequence_bit_exact(gpu, rnd0, seed):
     r.close()
 
 
-@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("seed", range(max(6, SEEDS // 8)))
 def test_random_shards_sum_to_oracle(gpu, rnd0, seed):
     """A random scene cut into 2-8 interleaved bands of 1-24 rows (bdpt_set_shard), each band set
     rendered by its own context in the auto stream mode: every pixel is rendered by exactly one
