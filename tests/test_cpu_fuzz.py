@@ -6,7 +6,7 @@ import pytest
 
 import gpu_bidirectional_raytracer_amd as g
 import oracle
-from test_gpu_fuzz import NPASS, random_scene
+from test_gpu_fuzz import NPASS, SEEDS, random_scene
 
 W, H = 23, 17
 
@@ -16,7 +16,7 @@ def rnd0():
     return oracle.mt607(0)
 
 
-@pytest.mark.parametrize("seed", range(40))
+@pytest.mark.parametrize("seed", range(SEEDS))
 def test_cpu_backend_random_scene(rnd0, seed):
     cam, sp = random_scene(1000 + seed)
     g.update_camera(cam, W, H)
@@ -36,7 +36,7 @@ def test_cpu_backend_random_scene(rnd0, seed):
     assert np.array_equal(px, opx)
 
 
-@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("seed", range(max(6, SEEDS // 8)))
 def test_cpu_backend_random_large_scene(rnd0, seed):
     from test_gpu_fuzz import random_large_scene
     cam, sp = random_large_scene(2000 + seed)
