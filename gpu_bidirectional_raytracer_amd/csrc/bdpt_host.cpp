@@ -16,6 +16,7 @@
 #include <string.h>
 #include <sys/stat.h>
 #include <unistd.h>
+#include <algorithm>
 #include <map>
 #include <string>
 #include <vector>
@@ -89,24 +90,29 @@ struct bdpt_ctx {
     bool rand_ready = false;
     int shard = 0, nshards = 1, band_rows = 8;
     int streams_req = 0;                // bdpt_set_streams: 0 = auto (measured), -1 = one pass per lane
-    // auto mode: the first four calls of >= 2 passes run the pass-stream kernels, the fused S = 1
-    // kernel with paired segment loads (bdpt_kernels.hip BDPT_RNG_PAIR), the pass-stream kernels
-    // again and the fused kernel without pairing; the faster fused variant is kept only if its
-    // device time per pass beats the faster of the two pass-stream calls by kTuneMargin (a cold
-    // first call -- clocks still ramping -- no longer decides for the fused kernel).  tune_phase
-    // 0..3: measuring; 4: all issued; 5: decided.  Reset by scene / shard / traversal /
-    // specialisation / stream-mode changes.  BDPT_STREAMS_TUNE=0: no measurement.
+    // auto mode: the first six calls of >= 2 passes run, in this order, the pass-stream kernels
+    // with two passes per lane, the fused S = 1 kernel with paired segment loads (bdpt_kernels.hip
+    // BDPT_RNG_PAIR), pass streams with four passes per lane, two per lane again, the fused kernel
+    // without pairing and four per lane again.  The pass-stream variant kept is the one with the
+    // faster of its two calls (device time per pass); the faster fused variant replaces it only if
+    // it beats that by kTuneMargin (a cold first call -- clocks still ramping -- no longer decides
+    // for the fused kernel).  tune_phase 0..5: measuring; 6: all issued; 7: decided.  Reset by
+    // scene / shard / traversal / specialisation / stream-mode changes.  BDPT_STREAMS_TUNE=0: no
+    // measurement (two passes per lane).
     // (5 %: open scenes gain >= 10 % from the fused kernel, closed ones lose >= 7 %; with 2 % a
-    // one-call measurement once kept the fused kernel for gantz, 7 % slower, profiles/r03_s27_*)
+    // one-call measurement once kept the fused kernel for gantz, 7 % slower, profiles/r03_s27_*.
+    // Four passes per lane: cornell_glass / cornell_mirror +1.2 %, synthetic64 -2.8 % at 128-pass
+    // launches, profiles/r03_s45_ab_passes_per_lane.txt -- so it is measured, not fixed.)
     static constexpr double kTuneMargin = 0.05;
-    static constexpr int kTunePhases = 4;
+    static constexpr int kTunePhases = 6;
     bool tune_enabled = true;
     int tune_phase = 0;
     bool tune_fused = false;
     bool tune_pair = true;              // the fused variant kept: paired segment loads or not
-    long long tune_call[kTunePhases] = {-1, -1, -1, -1};
-    double tune_ms[kTunePhases] = {0.0, 0.0, 0.0, 0.0};
-    int tune_npass[kTunePhases] = {0, 0, 0, 0};
+    bool tune_quarter = false;          // the pass-stream variant kept: four passes per lane
+    long long tune_call[kTunePhases] = {-1, -1, -1, -1, -1, -1};
+    double tune_ms[kTunePhases] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    int tune_npass[kTunePhases] = {0, 0, 0, 0, 0, 0};
     int last_streams = 1;               // S of the last path-pass launch
     bool last_bvh = false;              // the last path-pass launch traversed the BVH
     int cus = 256;                      // compute units (auto stream count)
@@ -1052,17 +1058,19 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
     if (c->streams_req == 0 && c->tune_enabled) {
         if (c->tune_phase == bdpt_ctx::kTunePhases) {        // waits for the last measured call
             if (int rc = fold_timing(c, c->tune_call[bdpt_ctx::kTunePhases - 1] + 1)) return rc;
-            const double a0 = c->tune_ms[0] / c->tune_npass[0], a2 = c->tune_ms[2] / c->tune_npass[2];
-            const double fp = c->tune_ms[1] / c->tune_npass[1], fn = c->tune_ms[3] / c->tune_npass[3];
+            auto per = [&](int r) { return c->tune_ms[r] / c->tune_npass[r]; };
+            const double half = std::min(per(0), per(3)), quarter = std::min(per(2), per(5));
+            const double fp = per(1), fn = per(4);
             c->tune_pair = fp <= fn;
+            c->tune_quarter = quarter < half;
             const double fused = c->tune_pair ? fp : fn;
-            c->tune_fused = fused * (1.0 + bdpt_ctx::kTuneMargin) < (a0 < a2 ? a0 : a2);
+            c->tune_fused = fused * (1.0 + bdpt_ctx::kTuneMargin) < std::min(half, quarter);
             c->tune_phase = bdpt_ctx::kTunePhases + 1;
         }
         if (c->tune_phase < bdpt_ctx::kTunePhases && npass >= 2) {
             tune_role = c->tune_phase;
-            if (tune_role == 1 || tune_role == 3) S = 1;
-            pair = tune_role != 3;
+            if (tune_role == 1 || tune_role == 4) S = 1;
+            pair = tune_role != 4;
         } else if (c->tune_phase == bdpt_ctx::kTunePhases + 1 && c->tune_fused) {
             S = 1;
             pair = c->tune_pair;
@@ -1095,7 +1103,12 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
     // whose first path ends early start the second in groups, bdpt_kernels.hip BDPT_REGEN_STREAMS):
     // cornell +0.6 %, cornell_glass +1.7 %, cornell_mirror +1.5 %; not for BVH traversal
     // (complex -4.6 %: its lanes' traversal costs differ more than their path lengths)
-    if (c->streams_req == 0 && S >= 4 && !bvh) S = (S + 1) / 2;
+    // (four passes per lane when the measurement chose them, or to measure them; launches of >= 8)
+    if (c->streams_req == 0 && S >= 4 && !bvh) {
+        const bool quarter = tune_role >= 0 ? (tune_role == 2 || tune_role == 5)
+                                            : (c->tune_phase == bdpt_ctx::kTunePhases + 1 && c->tune_quarter);
+        S = quarter && S >= 8 ? (S + 3) / 4 : (S + 1) / 2;
+    }
     c->last_streams = S;
     const int kidx = bvh ? 17 : (a.n <= 16 ? (int)a.n : 0);
     if (bvh) {

@@ -97,13 +97,15 @@ int  bdpt_set_shard(bdpt_ctx *ctx, int shard, int nshards, int band_rows);
 /* Pass streams (no reference counterpart; results are bit-identical for every S): S lanes per
  * pixel render passes s, s+S, ... into an HBM radiance buffer (12 B per pass and pixel) and an
  * ordered fold applies the running mean of device.cu:774-787 in pass order.
- *   0  = auto (default): the first four calls of >= 2 passes run the pass-stream kernel (one
- *        pass per lane; two per lane, S = ceil(passes / 2), in launches of >= 4 passes that do
- *        not use the BVH), the fused kernel with paired segment loads, the pass-stream kernel
- *        again and the fused kernel without pairing; later calls use the faster fused variant
- *        only if its device time per pass beat both pass-stream calls by 5 % (closed scenes with
- *        long paths favour pass streams, open scenes with short paths the fused kernel);
- *        re-measured after a scene / shard / traversal change;
+ *   0  = auto (default): the first six calls of >= 2 passes measure, in this order, the
+ *        pass-stream kernel with two passes per lane (S = ceil(passes / 2); one per lane in
+ *        launches of < 4 passes or with the BVH), the fused kernel with paired segment loads,
+ *        pass streams with four passes per lane (S = ceil(passes / 4), launches of >= 8), two
+ *        per lane again, the fused kernel without pairing and four per lane again; later calls
+ *        use the pass-stream variant with the faster of its two calls, or the faster fused
+ *        variant if its device time per pass beat that by 5 % (closed scenes with long paths
+ *        favour pass streams, open scenes with short paths the fused kernel); re-measured after
+ *        a scene / shard / traversal change;
  *  -1  = BDPT_STREAMS_PER_LANE: always one pass per lane (S = passes per launch, <= 128);
  *   1  = the fused kernel that keeps the running mean in registers (no buffer);
  *  2..128 = that many streams. */

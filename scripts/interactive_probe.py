@@ -34,9 +34,9 @@ def main():
         r.path_passes(sid[k:k + 1], vlp[k:k + 1])
     # the multi-pass call below resolves (compiles) the pass-stream kernel and runs the auto mode's
     # measured calls: do that untimed, then reset the mode so one-pass calls stay fused
-    for k in range(5):
-        b = 10 + 3 * args.calls + k * (args.calls // 5)
-        r.path_passes(sid[b:b + args.calls // 5], vlp[b:b + args.calls // 5])
+    for k in range(7):
+        b = 10 + 3 * args.calls + k * (args.calls // 7)
+        r.path_passes(sid[b:b + args.calls // 7], vlp[b:b + args.calls // 7])
     out = {"W": W, "H": H, "calls": args.calls}
     for mode in ("pass", "pass+pixels"):
         base = 10 if mode == "pass" else 10 + args.calls

@@ -2,7 +2,7 @@
 
 For each N, the first and last rank's share of an N-way band shard (1/N of the rows; N x passes
 for weak scaling, the same passes with --strong) is rendered on one GPU with auto pass streams
-(after the auto mode's four measured calls) and with the S values asked for, and its device time
+(after the auto mode's six measured calls) and with the S values asked for, and its device time
 is compared with the N = 1 step: efficiency = t(N=1) / t(rank share), over N for --strong.  The
 RCCL reduce is not included (it runs once per frame, not per step).
 
@@ -20,7 +20,7 @@ sys.path.insert(0, REPO)
 import gpu_bidirectional_raytracer_amd as g  # noqa: E402
 
 
-WARM = 5
+WARM = 7
 
 
 def run(sp, cam, W, H, sid, vlp, shard, nshards, band, streams, reps):
@@ -29,7 +29,7 @@ def run(sp, cam, W, H, sid, vlp, shard, nshards, band, streams, reps):
     r.set_streams(streams)
     r.light_pass(0)
     n = len(sid) // (reps + WARM)
-    for k in range(WARM):                               # warm-up (the auto mode measures 4 calls)
+    for k in range(WARM):                               # warm-up (the auto mode measures 6 calls)
         r.path_passes(sid[k * n:(k + 1) * n], vlp[k * n:(k + 1) * n])
     r.synchronize()
     r.path_timing(reset=True)

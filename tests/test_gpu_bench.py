@@ -22,12 +22,14 @@ def run_bench(*args):
 
 
 def test_bench_crosses_counter_cap():
-    # (4 tuning + 1 warm-up + 240 timed) x 128 passes = 31,360 > 30,000: one reset
+    # (tuning + 1 warm-up + 240 timed steps) x 128 passes > 30,000: one reset
     d = run_bench("--scene", "simple", "--width", "96", "--height", "64", "--passes", "128",
                   "--steps", "240", "--warmup", "1", "--no-cpu-baseline")
     cfg = d["config"]
+    steps = d["tune_steps"] + 1 + 240
+    assert 30000 < steps * 128 < 2 * 30000
     assert cfg["accum_resets"] == 1
-    assert cfg["spp_total"] == 245 * 128 - 30000 // 128 * 128
+    assert cfg["spp_total"] == steps * 128 - 30000 // 128 * 128
     assert d["n_gpus"] == 1 and d["steps"] == 240 and d["value"] > 0
     assert cfg["samples_per_step"] == 97 * 65 * 128
     for k in ("metric", "unit", "ms_per_step", "higher_is_better", "scaling", "dtype", "roofline", "cpu_baseline"):

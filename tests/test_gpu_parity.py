@@ -204,37 +204,34 @@ def test_per_lane_streams_policy(gpu):
 
 @pytest.mark.parametrize("name", ["cornell", "caustic"])
 def test_auto_streams_measured(gpu, rnd0, name):
-    """Auto (0): the first four calls of >= 2 passes run pass streams (two passes per lane in
-    launches of >= 4 passes), the fused kernel with paired segment loads, pass streams again and
-    the fused kernel without pairing; later calls use the faster fused variant only if it measured
-    faster than both pass-stream calls; a scene change measures again.  Every call's result is the
+    """Auto (0): the first six calls of >= 2 passes run pass streams with two passes per lane
+    (launches of >= 4 passes), the fused kernel with paired segment loads, pass streams with four
+    passes per lane (launches of >= 8), two per lane again, the fused kernel without pairing and
+    four per lane again; later calls use the faster pass-stream variant, or the faster fused one
+    if it measured faster still; a scene change measures again.  Every call's result is the
     oracle's whatever was chosen."""
     W, H = 97, 65
     r, cam, sp = make(name, W, H, gpu)
-    sid, vlp = schedule(64)
+    sid, vlp = schedule(80)
     r.path_passes(sid[:1], vlp[:1])                        # 1 pass: not a measurement
     assert r.last_streams == 1
-    r.path_passes(sid[1:9], vlp[1:9])
-    assert r.last_streams == 4                             # measures pass streams (2 per lane)
-    r.path_passes(sid[9:17], vlp[9:17])
-    assert r.last_streams == 1                             # measures the fused kernel (paired loads)
-    r.path_passes(sid[17:25], vlp[17:25])
-    assert r.last_streams == 4                             # pass streams again
-    r.path_passes(sid[25:33], vlp[25:33])
-    assert r.last_streams == 1                             # the fused kernel without pairing
+    for k, want in enumerate((4, 1, 2, 4, 1, 2)):         # the six measured calls of 8 passes
+        a0 = 1 + 8 * k
+        r.path_passes(sid[a0:a0 + 8], vlp[a0:a0 + 8])
+        assert r.last_streams == want, (k, r.last_streams)
     used = []
-    for a0 in (33, 41):
+    for a0 in (49, 57):
         r.path_passes(sid[a0:a0 + 8], vlp[a0:a0 + 8])
         used.append(r.last_streams)
-    assert used[0] == used[1] and used[0] in (1, 4), used
+    assert used[0] == used[1] and used[0] in (1, 2, 4), used
     col, cnt = r.read_radiance()
     lp = oracle.light_pass(sp, rnd0, 0)
-    ocol, ocnt, opix = oracle.path_passes(sp, rnd0, cam, W, H, lp, sid[:49], vlp[:49])
+    ocol, ocnt, opix = oracle.path_passes(sp, rnd0, cam, W, H, lp, sid[:65], vlp[:65])
     assert_same(cnt, ocnt, "counter")
     assert_same(col, ocol, "colors")
     assert_same(r.read_pixels(), opix, "pixels")
     r.set_scene(sp)                                        # ReInitScene: measure again
-    r.path_passes(sid[49:56], vlp[49:56])
+    r.path_passes(sid[65:72], vlp[65:72])
     assert r.last_streams == 4                             # 7 passes, two per lane
     r.close()
 
