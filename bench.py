@@ -293,7 +293,7 @@ def smt_yield(scene, W, H, y0, sid, vlp, seconds, usable):
 
 def _pmc_record(name, workload, scene, W, H, passes_per_launch, streams, specialized):
     """The PMC record of profiles/<name> for this exact configuration (files hold one record per
-    workload), or None."""
+    workload and pass-stream count, keyed workload@S<streams>), or None."""
     path = os.path.join(REPO, "profiles", name)
     if not os.path.exists(path):
         return None

@@ -62,5 +62,5 @@ if len(sys.argv) > 4:
     data = json.load(open(out)) if os.path.exists(out) else {}
     if "scene" in data:                                   # an older single-record file
         data = {data.get("workload", "cornell1080"): data}
-    data[rec["workload"]] = rec
+    data[f'{rec["workload"]}@S{rec["pass_streams"]}'] = rec      # one record per workload and stream count
     json.dump(data, open(out, "w"), indent=1)

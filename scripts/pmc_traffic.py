@@ -72,11 +72,11 @@ rec = {"workload": cfg.get("workload", "cornell1080").split(":")[0], "scene": cf
        "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), x1024, calibrated",
        "method": __doc__}
 os.makedirs(os.path.dirname(out), exist_ok=True)
-# one record per workload: {workload: record}
+# one record per workload and pass-stream count: {workload@S<streams>: record}
 data = json.load(open(out)) if os.path.exists(out) else {}
 if "scene" in data:                                       # an older single-record file
     data = {data.get("workload", "cornell1080"): data}
-data[rec["workload"]] = rec
+data[f'{rec["workload"]}@S{rec["pass_streams"]}'] = rec      # one record per workload and stream count
 json.dump(data, open(out, "w"), indent=1)
 print(json.dumps({k: v for k, v in rec.items() if k not in ("method", "calibration")}))
 print(json.dumps(calib))

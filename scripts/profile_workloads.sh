@@ -5,6 +5,8 @@
 # passes per lane; 1: fused);
 # the last two passes split the VALU instructions by class (scripts/valu_weighted.py).
 #   WORKLOADS="cornell1080:64 caustic8:1 weak64:32" bash scripts/profile_workloads.sh
+# An entry w:S:name profiles workload w at S streams under the output name `name` (e.g.
+# cornell1080:32:cornell1080s32 next to cornell1080:64, for both outcomes of the auto mode).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out; export TMPDIR=/tmp
@@ -20,19 +22,19 @@ PMC_SETS=(
   "SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE"
 )
 for ws in ${WORKLOADS:-cornell1080:64 caustic8:1 weak64:32}; do
-  w=${ws%%:*}; S=${ws##*:}
+  IFS=: read -r w S name <<< "$ws"; name=${name:-$w}
   steps=${STEPS_STATS:-10}
   [ "$w" = weak64 ] && steps=${STEPS_STATS64:-6}
-  rm -rf gpurun_out/prof_$w
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$w -o run --output-format csv -- \
-      python3 bench.py --workload $w --no-cpu-baseline --steps $steps --warmup 3 > gpurun_out/prof_$w.log 2>&1 || stop "stats $w" $?
-  echo "stats $w: $(grep '^{' gpurun_out/prof_$w.log | tail -1 | cut -c1-200)"
+  rm -rf gpurun_out/prof_$name
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$name -o run --output-format csv -- \
+      python3 bench.py --workload $w --no-cpu-baseline --steps $steps --warmup 3 > gpurun_out/prof_$name.log 2>&1 || stop "stats $name" $?
+  echo "stats $name: $(grep '^{' gpurun_out/prof_$name.log | tail -1 | cut -c1-200)"
   i=0
   for set in "${PMC_SETS[@]}"; do
-    i=$((i+1)); rm -rf gpurun_out/pmc_${w}_$i
-    timeout -s KILL 240 rocprofv3 --pmc $set --kernel-trace -d gpurun_out/pmc_${w}_$i -o run --output-format csv -- \
-        python3 bench.py --workload $w --no-cpu-baseline --no-smt-probe --steps 4 --warmup 1 --streams $S > gpurun_out/pmc_${w}_$i.log 2>&1 || stop "pmc $w $i" $?
-    echo "pmc $w set $i ok"
+    i=$((i+1)); rm -rf gpurun_out/pmc_${name}_$i
+    timeout -s KILL 240 rocprofv3 --pmc $set --kernel-trace -d gpurun_out/pmc_${name}_$i -o run --output-format csv -- \
+        python3 bench.py --workload $w --no-cpu-baseline --no-smt-probe --steps 4 --warmup 1 --streams $S > gpurun_out/pmc_${name}_$i.log 2>&1 || stop "pmc $name $i" $?
+    echo "pmc $name set $i ok"
   done
 done
 echo PROFILE_DONE
