@@ -55,3 +55,15 @@ def test_gpus_2_without_gpus_refuses_cleanly():
 def test_smt_topology_helpers():
     topo = bench.cpu_topology()
     assert topo and all(isinstance(v, tuple) and len(v) == 2 for v in topo.values())
+
+
+def test_pmc_records_cover_both_auto_outcomes_of_the_headline():
+    """bench.py's roofline PMC fields come from profiles/pmc_{valu,traffic}.json for the exact
+    configuration run; the auto mode keeps two or four passes per lane on cornell1080 (64 or 32
+    streams at 128-pass launches), so both outcomes must have a record of each kind."""
+    for streams in (64, 32):
+        for name in ("pmc_valu.json", "pmc_traffic.json"):
+            rec = bench._pmc_record(name, "cornell1080", "cornell", 1921, 1081, 128.0, streams, True)
+            assert rec is not None, (name, streams)
+            assert rec["pass_streams"] == streams
+    assert bench._pmc_record("pmc_valu.json", "cornell1080", "cornell", 1921, 1081, 128.0, 16, True) is None
