@@ -308,6 +308,33 @@ def _pmc_record(name, workload, scene, W, H, passes_per_launch, streams, special
     return None
 
 
+def scaling_breakdown(per_dev, steps, dt, render_s, reduce_s, scaling, passes_per_step):
+    """Where a multi-GPU step's time goes, from per-device accumulators.
+
+    per_dev: one dict per GPU {kernel_ms, path_ms, launches, owned_pixels, ...} over the `steps`
+    timed steps (path_ms = path kernels + the pass-stream fold, device events).  dt = the
+    max-over-ranks wall time of the timed region, render_s = its part before the frame reduce
+    (max over ranks), reduce_s = the reduce (max over ranks).  For weak scaling every GPU holds
+    the per-GPU work of the one-GPU run, so the mean device's path time is the estimate of what
+    one GPU alone would take: weak_efficiency_vs_1gpu_estimate = that / dt.  Load imbalance is
+    the slowest device's path time over the mean."""
+    ps = [max(float(d["path_ms"]), 0.0) for d in per_dev]
+    mean_p = sum(ps) / max(len(ps), 1)
+    max_p = max(ps) if ps else 0.0
+    out = {"per_device": [dict(d, kernel_ms_per_step=round(d["kernel_ms"] / steps, 4),
+                               path_ms_per_step=round(d["path_ms"] / steps, 4),
+                               samples_per_step=int(d["owned_pixels"]) * passes_per_step) for d in per_dev],
+           "render_s": round(render_s, 6), "reduce_s": round(reduce_s, 6),
+           "reduce_frac": round(reduce_s / dt, 5) if dt > 0 else None,
+           "imbalance_max_over_mean": round(max_p / mean_p, 5) if mean_p > 0 else None,
+           "host_gap_frac": round(max(render_s - max_p / 1e3, 0.0) / dt, 5) if dt > 0 else None}
+    if scaling == "weak" and dt > 0:
+        out["weak_efficiency_vs_1gpu_estimate"] = round(mean_p / 1e3 / dt, 4)
+        out["weak_efficiency_note"] = ("mean device path time (one GPU's share = the one-GPU run's work) / "
+                                       "the job's wall time; 1 - it = imbalance + reduce + host gaps")
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1,
@@ -327,6 +354,8 @@ def main():
     ap.add_argument("--specialize", type=int, default=1, choices=[0, 1],
                     help="scene-specialised kernels (run-time compiled; results identical)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--tail-seconds", type=float, default=6.0,
+                    help="untimed GPU work after the timed steps (so an outside sampler sees the GPU busy)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-smt-probe", action="store_true", help="skip the SMT-yield probe of the CPU baseline")
     ap.add_argument("--rehearse", action="store_true",
@@ -374,6 +403,37 @@ def main():
         raise SystemExit(f"workload {args.workload} has {nshards} bands: at most {nshards} GPUs")
     cam, sp = g.read_scene(os.path.join(REPO, "assets", "scenes", wl["scene"] + ".scn"))
     g.update_camera(cam, W, H)
+    sched = g.PassScheduler()
+    sched.light()
+    per_step = wl["passes"] * (units if (wl["scaling"] == "weak" and not wl["fixed_bands"]) else 1)
+    # the auto stream mode measures its candidates on the first six calls (bdpt.h
+    # bdpt_set_streams): untimed extra steps when --warmup is shorter, so the timed steps run the
+    # kernel it settled on
+    tune = max(0, 7 - args.warmup) if args.streams == 0 else 0
+    untimed = tune + args.warmup
+    sid, vlp = sched.next(per_step * (untimed + args.steps))
+
+    # The CPU baseline (rank 0 at N = 1) runs first, before the GPU is touched: the GPU phase
+    # (tuning, warm-up, timed steps, untimed tail) then runs as one block an outside sampler sees.
+    cpu = None
+    if world == 1 and ndev == 1 and not args.no_cpu_baseline:
+        rows = shd.owned_row_ranges(H, rank, nshards, band)
+        region = (rows[0][0], rows[0][1]) if wl["fixed_bands"] else (0, H)
+        cpu = cpu_baseline(sp, cam, W, H, region, sid, vlp, args.cpu_seconds)
+        if not args.no_smt_probe:
+            mid = region[0] + (region[1] - region[0]) // 3
+            smt = smt_yield(wl["scene"], W, H, mid, sid, vlp, max(2.0, args.cpu_seconds / 4), cpu["cores"])
+            cpu["smt"] = smt
+            if smt and smt.get("smt_yield") and smt.get("node_physical_cores"):
+                # the verdict's node model: physical cores x 1-core rate x SMT yield
+                cpu["node_estimate"] = round(smt["node_physical_cores"] * cpu["value_1core"] * smt["smt_yield"], 2)
+                cpu["node_estimate_note"] = ("physical cores of the node x the 1-core rate (value_1core, same "
+                                             "frame) x the SMT yield (k cores with both siblings busy / the "
+                                             "same k cores with one thread each, same rows); assumes every "
+                                             "core keeps the 1-core rate (no memory-bandwidth limit), so it "
+                                             "is still an upper estimate of the whole host")
+        cpu["order"] = "run before the GPU phase (no GPU work in flight)"
+
     if mode == "inproc":
         devices = dev_list or list(range(ndev))
         r = g.Renderer(sp, W, H, cam, devices=devices)
@@ -388,15 +448,6 @@ def main():
     r.set_streams(args.streams)
     r.set_specialize(bool(args.specialize))
     r.light_pass(0)                                           # UpdateRendering2
-    sched = g.PassScheduler()
-    sched.light()
-    per_step = wl["passes"] * (units if (wl["scaling"] == "weak" and not wl["fixed_bands"]) else 1)
-    # the auto stream mode measures its candidates on the first six calls (bdpt.h
-    # bdpt_set_streams): untimed extra steps when --warmup is shorter, so the timed steps run the
-    # kernel it settled on
-    tune = max(0, 7 - args.warmup) if args.streams == 0 else 0
-    untimed = tune + args.warmup
-    sid, vlp = sched.next(per_step * (untimed + args.steps))
     # samples per step over the whole job: every owned pixel of every GPU, once per pass
     job_pixels = sum(shd.owned_pixels(W, H, q, nshards, band) for q in range(units))
     own_pixels = shd.owned_pixels(W, H, rank, nshards, band)  # this rank's (or device 0's) share
@@ -445,20 +496,25 @@ def main():
     for k in range(untimed, untimed + args.steps):
         step(k)
     r.synchronize()
+    t_render = time.perf_counter()                            # rendering done; the reduce is timed apart
     if dist is not None:                                      # assemble the frame on rank 0
         shd.reduce_frame(t_col, t_cnt, dst=0)
     elif mode == "inproc":                                    # in-process RCCL reduce to device 0
         r.reduce_frame()
     torch.cuda.synchronize()
+    t_reduce = time.perf_counter()
     barrier()
     dt = time.perf_counter() - t0
+    render_s, reduce_s = t_render - t0, t_reduce - t_render
     if dist is not None:
-        tt = torch.tensor([dt], device="cpu" if args.rehearse else f"cuda:{local}", dtype=torch.float64)
+        tt = torch.tensor([dt, render_s, reduce_s], device="cpu" if args.rehearse else f"cuda:{local}",
+                          dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
+        dt, render_s, reduce_s = (float(x) for x in tt.tolist())
 
     kern_ms, launches = r.kernel_timing()                     # path kernels alone
     dev_ms, _ = r.path_timing()                               # + the pass-stream fold
+    per_dev = r.device_timing()                               # each device's own share (no max)
     samples = job_pixels * per_step * args.steps
     value = samples / dt / 1e6
     ident = gpu_identity(local)
@@ -467,11 +523,19 @@ def main():
         gathered = [None] * world
         dist.all_gather_object(gathered, ident)
         idents = gathered
+        mine = dict(per_dev[0], rank=rank)
+        gathered = [None] * world
+        dist.all_gather_object(gathered, mine)
+        per_dev = gathered
     elif mode == "inproc":
         idents = [gpu_identity(d) for d in devices]
+    scaling = scaling_breakdown(per_dev, args.steps, dt, render_s, reduce_s, wl["scaling"], per_step)
 
+    # Untimed tail: keep the GPU busy for a few seconds after the clock stops, so an outside
+    # utilisation sampler sees the device working (the timed region alone is well under a second
+    # at 1080p).  Its passes are not counted anywhere; the frame is checked below before it runs.
+    spp_total = held[0]                                       # passes since the last reset
     if rank == 0:
-        spp_total = held[0]                                   # passes since the last reset
         # check the (assembled) frame's counters: every rendered pixel holds every pass since the
         # last reset, the rest none
         if dist is not None:
@@ -481,6 +545,26 @@ def main():
             cnt = r.read_radiance()[1]
         owned = (torch.arange(H).numpy() // band) % nshards < units
         assert (cnt[owned] == spp_total).all() and (cnt[~owned] == 0).all(), "frame counters wrong"
+    tail_s, tail_steps = max(0.0, args.tail_seconds), 0
+    if tail_s > 0:
+        t1 = time.perf_counter()
+        step_s = max(dt / max(args.steps, 1), 1e-4)
+        k = untimed + args.steps
+        tsid, tvlp = sched.next(per_step * 8)                 # the same pass tables, reused per tail step
+        while time.perf_counter() - t1 < tail_s and tail_steps < 100000:
+            burst = max(1, min(8, int((tail_s - (time.perf_counter() - t1)) / step_s) + 1))
+            for _ in range(burst):
+                if held[0] + per_step > COUNTER_CAP:
+                    r.reset_accum()
+                    held[0] = 0
+                r.path_passes(tsid[:per_step], tvlp[:per_step], sync=False)
+                held[0] += per_step
+                tail_steps += 1
+            r.synchronize()
+        barrier()
+        tail_s = time.perf_counter() - t1
+
+    if rank == 0:
         w = WORK.get(wl["scene"])
         avg_launch_s = kern_ms / 1e3 / max(launches, 1)
         passes_per_launch = per_step * args.steps / max(launches, 1)
@@ -502,6 +586,9 @@ def main():
             skips = [f for f in features if f in ("det_skip", "zero_exit", "last_skip", "bvh")]
             roofline = {"bound": "valu", "achieved": round(fl, 3), "peak": FP32_NOFMA_TFLOPS, "unit": "TFLOP/s",
                         "frac": round(fl / FP32_NOFMA_TFLOPS, 4),
+                        "frac_spec": round(fl / FP32_PEAK_TFLOPS, 4),
+                        "frac_note": "frac is against the 78.6 T one-op-per-lane-cycle ceiling (no FMA "
+                                     "contraction); frac_spec against the 157.3 TFLOP/s fp32 spec (FMA = 2 FLOP)",
                         "traffic": trec.get("hbm_bytes_per_launch") if trec else None,
                         "peak_fma": FP32_PEAK_TFLOPS, "frac_fma": round(fl / FP32_PEAK_TFLOPS, 4),
                         "flop_per_sample": round(flop_per_sample(w), 1),
@@ -529,23 +616,6 @@ def main():
                     if k in vrec:
                         roofline[{"valu_busy": "valu_busy_pmc",
                                   "valu_lane_utilisation": "lane_utilisation_pmc"}.get(k, k + "_pmc")] = vrec[k]
-        cpu = None
-        if world == 1 and ndev == 1 and not args.no_cpu_baseline:
-            rows = shd.owned_row_ranges(H, rank, nshards, band)
-            region = (rows[0][0], rows[0][1]) if wl["fixed_bands"] else (0, H)
-            cpu = cpu_baseline(sp, cam, W, H, region, sid, vlp, args.cpu_seconds)
-            if not args.no_smt_probe:
-                mid = region[0] + (region[1] - region[0]) // 3
-                smt = smt_yield(wl["scene"], W, H, mid, sid, vlp, max(2.0, args.cpu_seconds / 4), cpu["cores"])
-                cpu["smt"] = smt
-                if smt and smt.get("smt_yield") and smt.get("node_physical_cores"):
-                    # the verdict's node model: physical cores x 1-core rate x SMT yield
-                    cpu["node_estimate"] = round(smt["node_physical_cores"] * cpu["value_1core"] * smt["smt_yield"], 2)
-                    cpu["node_estimate_note"] = ("physical cores of the node x the 1-core rate (value_1core, same "
-                                                 "frame) x the SMT yield (k cores with both siblings busy / the "
-                                                 "same k cores with one thread each, same rows); assumes every "
-                                                 "core keeps the 1-core rate (no memory-bandwidth limit), so it "
-                                                 "is still an upper estimate of the whole host")
         if mode == "ranks":
             reduce_backend = "gloo (torch.distributed, host-staged)" if args.rehearse else "rccl (torch.distributed nccl)"
         elif mode == "inproc":
@@ -574,6 +644,10 @@ def main():
             "devices": [{"rank": q, **idents[q]} for q in range(len(idents))] if mode == "ranks"
             else [{"device": d, **idents[i]} for i, d in enumerate(devices)],
             "device_ms_per_step": round(dev_ms / args.steps, 3),
+            "scaling_breakdown": scaling,
+            "untimed_tail": {"seconds": round(tail_s, 2), "steps": tail_steps,
+                             "note": "GPU work after the timed region, not counted: keeps the device visibly "
+                                     "busy for an outside sampler"},
             "roofline": roofline, "cpu_baseline": cpu,
             "host": {"gpu": ident.get("name"), "hostname": socket.gethostname(), "gpu_pci": ident.get("pci"),
                      "gpu_unique_id": ident.get("unique_id")},

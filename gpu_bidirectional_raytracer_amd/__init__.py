@@ -301,6 +301,19 @@ class Renderer:
         self._chk(lib.bdpt_kernel_timing(self._h, ctypes.byref(ms), ctypes.byref(n), int(reset)))
         return ms.value, n.value
 
+    def device_timing(self) -> list:
+        """Per device of the context (devices[0] first): {device, kernel_ms, path_ms, launches,
+        owned_pixels} since the last timing reset (bdpt_device_timing; no reset)."""
+        out = []
+        for k in range(self.num_devices):
+            d, km, pm = ctypes.c_int(), ctypes.c_double(), ctypes.c_double()
+            n, own = ctypes.c_longlong(), ctypes.c_longlong()
+            self._chk(lib.bdpt_device_timing(self._h, k, ctypes.byref(d), ctypes.byref(km), ctypes.byref(pm),
+                                             ctypes.byref(n), ctypes.byref(own)))
+            out.append({"device": d.value, "kernel_ms": km.value, "path_ms": pm.value,
+                        "launches": n.value, "owned_pixels": own.value})
+        return out
+
     def update_pixels(self) -> None:
         self._chk(lib.bdpt_update_pixels(self._h))
 
@@ -322,9 +335,15 @@ class Renderer:
         self._chk(lib.bdpt_save_checkpoint(self._h, os.fsencode(path), buf, len(host_state)))
 
     def load_checkpoint(self, path: str, host_bytes: int = 0) -> bytes:
-        """Restore the accumulation; returns the caller state saved with it (host_bytes long)."""
+        """Restore the render state saved with the frame -- scene, camera, MT table (by its seed),
+        VLPs -- and the accumulation (bdpt_load_checkpoint); self.spheres and self.camera follow
+        the restored values.  Returns the caller state saved with it (host_bytes long)."""
         buf = ctypes.create_string_buffer(host_bytes) if host_bytes else None
         self._chk(lib.bdpt_load_checkpoint(self._h, os.fsencode(path), buf, host_bytes))
+        self.spheres = self.get_scene()
+        cam = self.get_camera()
+        if cam is not None:
+            self.camera = cam
         return buf.raw if buf is not None else b""
 
     def read_pixels(self) -> np.ndarray:

@@ -80,6 +80,9 @@ _SIGS = [
     ("bdpt_specialize_status", ctypes.c_char_p, [_P]),
     ("bdpt_set_traversal", ctypes.c_int, [_P, ctypes.c_int]),
     ("bdpt_kernel_timing", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong), ctypes.c_int]),
+    ("bdpt_device_timing", ctypes.c_int, [_P, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+                                          ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                          ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_longlong)]),
     ("bdpt_scene_has_bvh", ctypes.c_int, [_P]),
     ("bdpt_last_traversal", ctypes.c_int, [_P]),
     ("bdpt_last_kernel_features", ctypes.c_int, [_P]),

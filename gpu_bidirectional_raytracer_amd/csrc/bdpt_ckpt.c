@@ -33,6 +33,7 @@
 int bdpt__fail(bdpt_ctx *c, int code, const char *msg);
 
 static const char kMagic[8] = {'B', 'D', 'P', 'T', 'C', 'K', 'P', '2'};
+static const char kMagicV1[8] = {'B', 'D', 'P', 'T', 'C', 'K', 'P', '1'};   /* round-2 format */
 enum { kHasRand = 1, kHasCamera = 2 };
 
 typedef struct {
@@ -124,6 +125,50 @@ int bdpt_save_checkpoint(bdpt_ctx *c, const char *path, const void *host_state, 
     return rc;
 }
 
+/* The context's own render state, kept so a load that fails half way can put it back. */
+typedef struct {
+    int n, has_cam, has_rand;
+    unsigned seed;
+    bdpt_camera cam;
+    bdpt_sphere *sp;
+    bdpt_lightpath *lp;
+    bdpt_vec *col;
+    unsigned *cnt;
+} ctx_state;
+
+static void state_free(ctx_state *s)
+{
+    free(s->sp); free(s->lp); free(s->col); free(s->cnt);
+}
+
+static int state_save(bdpt_ctx *c, ctx_state *s, size_t np)
+{
+    memset(s, 0, sizeof *s);
+    s->n = bdpt_get_scene(c, NULL, 0);
+    if (s->n < 0) return s->n;
+    s->has_cam = bdpt_get_camera(c, &s->cam) == BDPT_OK;
+    s->has_rand = bdpt_rand_seed(c, &s->seed) == BDPT_OK;
+    s->sp = malloc(sizeof(bdpt_sphere) * (s->n ? s->n : 1));
+    s->lp = malloc(sizeof(bdpt_lightpath) * BDPT_LIGHT_POINTS);
+    s->col = malloc(sizeof(bdpt_vec) * np);
+    s->cnt = malloc(sizeof(unsigned) * np);
+    if (!(s->sp && s->lp && s->col && s->cnt)) return BDPT_ENOMEM;
+    if (bdpt_get_scene(c, s->sp, (unsigned)s->n) != s->n) return BDPT_ESTATE;
+    int rc = bdpt_read_lightpaths(c, s->lp);
+    if (rc == BDPT_OK) rc = bdpt_read_radiance(c, s->col, s->cnt);
+    return rc;
+}
+
+/* Put the saved state back (best effort: the first failure is the caller's error). */
+static void state_restore(bdpt_ctx *c, const ctx_state *s)
+{
+    if (bdpt_set_scene(c, s->sp, (unsigned)s->n) != BDPT_OK) return;
+    if (s->has_cam && bdpt_set_camera(c, &s->cam) != BDPT_OK) return;
+    if (s->has_rand && bdpt_generate_rand(c, s->seed) != BDPT_OK) return;
+    if (bdpt_write_lightpaths(c, s->lp) != BDPT_OK) return;
+    (void)bdpt_write_radiance(c, s->col, s->cnt);
+}
+
 int bdpt_load_checkpoint(bdpt_ctx *c, const char *path, void *host_state, unsigned host_bytes)
 {
     if (!c || !path || (host_bytes && !host_state)) return BDPT_EINVAL;
@@ -132,7 +177,16 @@ int bdpt_load_checkpoint(bdpt_ctx *c, const char *path, void *host_state, unsign
     FILE *f = fopen(path, "rb");
     if (!f) return failf(c, BDPT_EIO, "bdpt_load_checkpoint: cannot open %s%s", path, "");
     ckpt_header h;
-    if (fread(&h, sizeof h, 1, f) != 1 || memcmp(h.magic, kMagic, 8) != 0) {
+    if (fread(&h, sizeof h, 1, f) != 1) {
+        fclose(f);
+        return failf(c, BDPT_EIO, "bdpt_load_checkpoint: %s is not a checkpoint%s", path, "");
+    }
+    if (memcmp(h.magic, kMagicV1, 8) == 0) {
+        fclose(f);
+        return failf(c, BDPT_EINVAL, "bdpt_load_checkpoint: %s is a version-1 checkpoint (BDPTCKP1: the frame "
+                     "without its scene, camera, table and VLPs), which this build cannot resume%s", path, "");
+    }
+    if (memcmp(h.magic, kMagic, 8) != 0) {
         fclose(f);
         return failf(c, BDPT_EIO, "bdpt_load_checkpoint: %s is not a checkpoint%s", path, "");
     }
@@ -158,13 +212,31 @@ int bdpt_load_checkpoint(bdpt_ctx *c, const char *path, void *host_state, unsign
           (host_bytes == 0 || fread(hs, 1, host_bytes, f) == host_bytes)))
         rc = failf(c, BDPT_EIO, "bdpt_load_checkpoint: %s is truncated%s", path, "");
     fclose(f);
-    /* restore in dependency order: scene (ReInitScene upload), camera, table, VLPs, frame */
-    if (rc == BDPT_OK) rc = bdpt_set_scene(c, sp, (unsigned)n);
-    if (rc == BDPT_OK && (h.flags & kHasCamera)) rc = bdpt_set_camera(c, &cam);
-    if (rc == BDPT_OK && (h.flags & kHasRand)) rc = bdpt_generate_rand(c, h.seed);
-    if (rc == BDPT_OK) rc = bdpt_write_lightpaths(c, lp);
-    if (rc == BDPT_OK) rc = bdpt_write_radiance(c, col, cnt);
+    /* the context's state before the load: put back if a restore step fails */
+    ctx_state old;
+    int saved = 0;
+    if (rc == BDPT_OK) {
+        rc = state_save(c, &old, np);
+        saved = 1;
+    }
+    /* restore in dependency order: scene (ReInitScene upload, skipped when the context already
+     * holds these spheres byte for byte: it would drop the specialised kernels and restart the
+     * stream-mode measurement), camera, table, VLPs, frame */
+    int step_rc = BDPT_OK;
+    if (rc == BDPT_OK && !((size_t)old.n == n && (n == 0 || memcmp(old.sp, sp, sizeof(bdpt_sphere) * n) == 0)))
+        rc = step_rc = bdpt_set_scene(c, sp, (unsigned)n);
+    if (rc == BDPT_OK && (h.flags & kHasCamera)) rc = step_rc = bdpt_set_camera(c, &cam);
+    if (rc == BDPT_OK && (h.flags & kHasRand)) rc = step_rc = bdpt_generate_rand(c, h.seed);
+    if (rc == BDPT_OK) rc = step_rc = bdpt_write_lightpaths(c, lp);
+    if (rc == BDPT_OK) rc = step_rc = bdpt_write_radiance(c, col, cnt);
+    if (step_rc != BDPT_OK) {                   /* a restore step failed: the old state back */
+        char msg[512];
+        snprintf(msg, sizeof msg, "%s", bdpt_last_error(c));
+        state_restore(c, &old);
+        (void)bdpt__fail(c, step_rc, msg);
+    }
     if (rc == BDPT_OK && host_bytes) memcpy(host_state, hs, host_bytes);
+    if (saved) state_free(&old);
     free(sp); free(lp); free(col); free(cnt); free(hs);
     return rc;
 }

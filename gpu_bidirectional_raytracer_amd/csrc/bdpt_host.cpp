@@ -17,6 +17,7 @@
 #include <sys/stat.h>
 #include <unistd.h>
 #include <algorithm>
+#include <limits>
 #include <map>
 #include <string>
 #include <vector>
@@ -112,6 +113,10 @@ struct bdpt_ctx {
     bool tune_quarter = false;          // the pass-stream variant kept: four passes per lane
     long long tune_call[kTunePhases] = {-1, -1, -1, -1, -1, -1};
     double tune_ms[kTunePhases] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    // whether each tuning call really ran its role's variant: four passes per lane needs launches
+    // of >= 8 passes, and the unpaired fused variant exists only as a specialised (JIT) build --
+    // otherwise the role repeated another role's kernel and must not decide anything
+    bool tune_real[kTunePhases] = {false, false, false, false, false, false};
     int tune_npass[kTunePhases] = {0, 0, 0, 0, 0, 0};
     int last_streams = 1;               // S of the last path-pass launch
     bool last_bvh = false;              // the last path-pass launch traversed the BVH
@@ -149,7 +154,7 @@ struct bdpt_ctx {
     int jit_waves = 0;                  // waves/SIMD bound of the last specialised build
     bool jit_zero_exit = false;         // the last specialised build has the black-surface exit
     // jit_path_kernel's answer per [pass streams][paired loads] for the current scene, specialise
-    // switch and BDPT_JIT_FLAGS: a call then resolves its kernel without rebuilding the option
+    // switch and JIT environment (jit_env_key): a call then resolves its kernel without rebuilding the option
     // strings (tens of microseconds per call, which the one-pass-per-call pattern pays every call)
     struct jit_memo_t {
         bool valid = false, zero_exit = false;
@@ -629,10 +634,22 @@ static void jit_forget(bdpt_ctx* c) {                   // the scene or the spec
         for (auto& m : row) m.valid = false;
 }
 
+// Every environment input of jit_path_kernel_build, as one memo key: an in-process A/B that
+// changes any of them gets a fresh build (BDPT_FUSED_MAX_PASSES is read once per process).
+static std::string jit_env_key() {
+    std::string k;
+    for (const char* v : {"BDPT_JIT_FLAGS", "BDPT_JIT_WAVES", "BDPT_JIT_FUSED_WAVES", "BDPT_JIT_SCRATCH_OK"}) {
+        const char* e = getenv(v);
+        k += e ? e : "";
+        k += '\x1f';
+    }
+    return k;
+}
+
 static hipFunction_t jit_path_kernel(bdpt_ctx* c, bool streams, bool pair = true) {
-    const char* jfl = getenv("BDPT_JIT_FLAGS");
+    const std::string key = jit_env_key();
     bdpt_ctx::jit_memo_t& m = c->jit_memo[streams][pair];
-    if (m.valid && strcmp(m.flags.c_str(), jfl ? jfl : "") == 0) {
+    if (m.valid && m.flags == key) {
         snprintf(c->jit_err, sizeof c->jit_err, "%s", m.err.c_str());
         if (m.fn) { c->jit_waves = m.waves; c->jit_zero_exit = m.zero_exit; }
         return m.fn;
@@ -642,7 +659,7 @@ static hipFunction_t jit_path_kernel(bdpt_ctx* c, bool streams, bool pair = true
     m.fn = fn;
     m.waves = c->jit_waves;
     m.zero_exit = c->jit_zero_exit;
-    m.flags = jfl ? jfl : "";
+    m.flags = key;
     m.err = c->jit_err;
     return fn;
 }
@@ -1058,10 +1075,11 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
     if (c->streams_req == 0 && c->tune_enabled) {
         if (c->tune_phase == bdpt_ctx::kTunePhases) {        // waits for the last measured call
             if (int rc = fold_timing(c, c->tune_call[bdpt_ctx::kTunePhases - 1] + 1)) return rc;
-            auto per = [&](int r) { return c->tune_ms[r] / c->tune_npass[r]; };
+            const double inf = std::numeric_limits<double>::infinity();
+            auto per = [&](int r) { return c->tune_real[r] ? c->tune_ms[r] / c->tune_npass[r] : inf; };
             const double half = std::min(per(0), per(3)), quarter = std::min(per(2), per(5));
             const double fp = per(1), fn = per(4);
-            c->tune_pair = fp <= fn;
+            c->tune_pair = !(fn < fp);                       // the default unless unpaired was measured faster
             c->tune_quarter = quarter < half;
             const double fused = c->tune_pair ? fp : fn;
             c->tune_fused = fused * (1.0 + bdpt_ctx::kTuneMargin) < std::min(half, quarter);
@@ -1104,10 +1122,12 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
     // cornell +0.6 %, cornell_glass +1.7 %, cornell_mirror +1.5 %; not for BVH traversal
     // (complex -4.6 %: its lanes' traversal costs differ more than their path lengths)
     // (four passes per lane when the measurement chose them, or to measure them; launches of >= 8)
+    bool quarter_ran = false;
     if (c->streams_req == 0 && S >= 4 && !bvh) {
         const bool quarter = tune_role >= 0 ? (tune_role == 2 || tune_role == 5)
                                             : (c->tune_phase == bdpt_ctx::kTunePhases + 1 && c->tune_quarter);
-        S = quarter && S >= 8 ? (S + 3) / 4 : (S + 1) / 2;
+        quarter_ran = quarter && S >= 8;
+        S = quarter_ran ? (S + 3) / 4 : (S + 1) / 2;
     }
     c->last_streams = S;
     const int kidx = bvh ? 17 : (a.n <= 16 ? (int)a.n : 0);
@@ -1233,6 +1253,9 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
     cs.launches = launches;
     cs.pending = true;
     if (tune_role >= 0) {
+        c->tune_real[tune_role] = tune_role == 2 || tune_role == 5 ? quarter_ran
+                                  : tune_role == 1 || tune_role == 4 ? (jf_fused != nullptr || tune_role == 1)
+                                  : true;
         c->tune_call[tune_role] = c->issued;
         c->tune_npass[tune_role] = npass;
         c->tune_phase = tune_role + 1;
@@ -1673,6 +1696,26 @@ int bdpt_kernel_timing(bdpt_ctx* c, double* kernel_ms, long long* launches, int 
         double ms = 0.0;
         if (int rc = one_kernel_timing(p, &ms, nullptr, reset)) return fail(c, rc, "device %d: %s", p->device, p->err);
         if (kernel_ms && ms > *kernel_ms) *kernel_ms = ms;
+    }
+    return BDPT_OK;
+}
+// One device of the group (k = 0 is devices[0]): its own accumulators, not the maximum, so a
+// multi-device run can show load imbalance.  Does not reset.
+int bdpt_device_timing(bdpt_ctx* c, int k, int* device, double* kernel_ms, double* path_ms,
+                       long long* launches, long long* owned_pixels) {
+    if (!c) return BDPT_EINVAL;
+    if (k < 0 || k > (int)c->peers.size())
+        return fail(c, BDPT_EINVAL, "bdpt_device_timing: device index %d of %d", k, 1 + (int)c->peers.size());
+    bdpt_ctx* d = k == 0 ? c : c->peers[k - 1];
+    if (int rc = one_synchronize(d)) return d == c ? rc : fail(c, rc, "device %d: %s", d->device, d->err);
+    if (device) *device = d->cpu ? BDPT_DEVICE_CPU : d->device;
+    if (kernel_ms) *kernel_ms = d->acc_kernel_ms;
+    if (path_ms) *path_ms = d->acc_ms;
+    if (launches) *launches = d->acc_launches;
+    if (owned_pixels) {
+        long long rows = 0;
+        for (int y = 0; y < d->H; y++) rows += (y / d->band_rows) % d->nshards == d->shard;
+        *owned_pixels = rows * d->W;
     }
     return BDPT_OK;
 }

@@ -170,6 +170,13 @@ int  bdpt_path_timing(bdpt_ctx *ctx, double *total_ms, long long *launches, int 
 /* Same accumulation, but only the path kernels' own durations (one HIP event pair around each
  * path-kernel launch, excluding the pass-stream fold): what rocprof reports for that kernel. */
 int  bdpt_kernel_timing(bdpt_ctx *ctx, double *kernel_ms, long long *launches, int reset);
+/* Device k of a (multi-device) context, 0 <= k < bdpt_num_devices (0 = devices[0]): its device
+ * id (BDPT_DEVICE_CPU for the host backend), its own path-kernel ms and path ms (with the fold)
+ * and launches since the last timing reset, and the pixels its shard owns.  Does not reset.
+ * New (the reference is single-device, smallpt_cpu.c:422): lets a multi-GPU run report each
+ * device's share instead of only the slowest. */
+int  bdpt_device_timing(bdpt_ctx *ctx, int k, int *device, double *kernel_ms, double *path_ms,
+                        long long *launches, long long *owned_pixels);
 
 /* Read-back.  colors/counter: the float parity artefact (dev_colors / dev_counter);
  * pixels: uchar4 RGBA = pixels_buf (SavePPM, smallpt_cpu.c:241). */
@@ -207,7 +214,10 @@ int  bdpt_write_radiance(bdpt_ctx *ctx, const bdpt_vec *colors, const unsigned *
  * camera, scene, MT table and VLPs, not the scene file's.  Written to a temporary file, flushed to
  * disk (fsync) and renamed into place.  Load checks W, H and host_bytes against the context, then
  * restores scene, camera, table, VLPs and accumulation (the caller re-reads its own copies with
- * bdpt_get_camera / bdpt_get_scene). */
+ * bdpt_get_camera / bdpt_get_scene).  The scene upload is skipped when the context already holds
+ * the same spheres byte for byte.  If a restore step fails, the context's previous scene, camera,
+ * table, VLPs and accumulation are put back (best effort) and the step's error is returned; a
+ * version-1 file ("BDPTCKP1", round 2) is refused with a message that says so. */
 int  bdpt_save_checkpoint(bdpt_ctx *ctx, const char *path, const void *host_state, unsigned host_bytes);
 int  bdpt_load_checkpoint(bdpt_ctx *ctx, const char *path, void *host_state, unsigned host_bytes);
 

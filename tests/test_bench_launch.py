@@ -67,3 +67,47 @@ def test_pmc_records_cover_both_auto_outcomes_of_the_headline():
             assert rec is not None, (name, streams)
             assert rec["pass_streams"] == streams
     assert bench._pmc_record("pmc_valu.json", "cornell1080", "cornell", 1921, 1081, 128.0, 16, True) is None
+
+
+def test_scaling_breakdown_fields():
+    """a multi-GPU line says where the time goes -- per-device kernel/path ms and
+    owned samples, the reduce apart from the render, imbalance and the weak-efficiency estimate."""
+    per_dev = [{"device": 0, "kernel_ms": 600.0, "path_ms": 640.0, "launches": 20, "owned_pixels": 1000},
+               {"device": 1, "kernel_ms": 660.0, "path_ms": 700.0, "launches": 20, "owned_pixels": 1000}]
+    s = bench.scaling_breakdown(per_dev, steps=20, dt=0.75, render_s=0.72, reduce_s=0.03, scaling="weak",
+                                passes_per_step=256)
+    assert [d["path_ms_per_step"] for d in s["per_device"]] == [32.0, 35.0]
+    assert [d["kernel_ms_per_step"] for d in s["per_device"]] == [30.0, 33.0]
+    assert s["per_device"][1]["samples_per_step"] == 256000
+    assert s["reduce_s"] == 0.03 and s["reduce_frac"] == 0.04
+    assert abs(s["imbalance_max_over_mean"] - 700 / 670) < 1e-4
+    assert abs(s["weak_efficiency_vs_1gpu_estimate"] - 0.67 / 0.75) < 1e-4
+    assert abs(s["host_gap_frac"] - 0.02 / 0.75) < 1e-4
+    strong = bench.scaling_breakdown(per_dev, 20, 0.75, 0.72, 0.03, "strong", 128)
+    assert "weak_efficiency_vs_1gpu_estimate" not in strong
+
+
+def test_device_timing_through_the_abi():
+    """bdpt_device_timing on a host-CPU context (the GPU contexts share the code): device id,
+    the context's own accumulators and the pixels its shard owns."""
+    import numpy as np
+    import gpu_bidirectional_raytracer_amd as g
+    from gpu_bidirectional_raytracer_amd import sharding as shd
+    from conftest import SCENES
+    W, H = 24, 40
+    cam, sp = g.read_scene(os.path.join(SCENES, "simple.scn"))
+    g.update_camera(cam, W, H)
+    with g.Renderer(sp, W, H, cam, device=-1) as r:
+        r.set_shard(1, 3, 8)
+        r.light_pass(0)
+        s = g.PassScheduler()
+        s.light()
+        sid, vlp = s.next(2)
+        r.path_passes(sid, vlp)
+        r.path_passes(sid, vlp)
+        (d,) = r.device_timing()
+        ms, n = r.kernel_timing()
+        assert d["device"] == -1 and d["launches"] == n == 2 and abs(d["kernel_ms"] - ms) < 1e-9
+        assert d["path_ms"] >= d["kernel_ms"] > 0
+        assert d["owned_pixels"] == shd.owned_pixels(W, H, 1, 3, 8) == 16 * W    # bands 1 and 4
+        assert g._lib.lib.bdpt_device_timing(r._h, 1, None, None, None, None, None) != 0   # one device only

@@ -233,3 +233,34 @@ def test_smallpt_host_resume_after_keys_matches_oracle_replay(tmp_path):
         for _ in range(3):
             ora.IdleFunc()
     assert np.array_equal(_read_ppm(out), ora.pixels[..., :3].astype(np.int64))
+
+
+def test_checkpoint_v1_refused_and_renderer_state_refreshed(rnd0, tmp_path):
+    """a round-2 (BDPTCKP1) file is refused with a version message, not 'not a
+    checkpoint'; Renderer.load_checkpoint refreshes its spheres/camera from the restored state; a
+    failed load leaves the context's frame as it was."""
+    W, H = 17, 11
+    sid, vlp = schedule(3)
+    r, cam, sp = make("cornell", W, H)
+    r.path_passes(sid, vlp)
+    edited = sp.copy()
+    edited["p"][8] += np.float32(2.0)                     # a sphere edit (ReInitScene) before the save
+    r.set_scene(edited)
+    r.save_checkpoint(str(tmp_path / "e.ckpt"))
+    before = r.read_radiance()
+    r.close()
+    v1 = tmp_path / "v1.ckpt"
+    v1.write_bytes(b"BDPTCKP1" + (tmp_path / "e.ckpt").read_bytes()[8:])
+    r2, _, _ = make("cornell", W, H)
+    r2.path_passes(sid, vlp)
+    mine = r2.read_radiance()
+    with pytest.raises(g.BdptError, match="version-1"):
+        r2.load_checkpoint(str(v1))
+    same(r2.read_radiance()[0], mine[0], "frame untouched by a refused load")
+    assert np.array_equal(r2.spheres.view(np.uint8), sp.view(np.uint8))
+    r2.load_checkpoint(str(tmp_path / "e.ckpt"))
+    assert np.array_equal(r2.spheres.view(np.uint8), edited.view(np.uint8))   # refreshed from the context
+    same(r2.read_radiance()[0], before[0], "restored frame")
+    r2.load_checkpoint(str(tmp_path / "e.ckpt"))          # same scene again: upload skipped, same result
+    same(r2.read_radiance()[0], before[0], "restored frame, scene unchanged")
+    r2.close()

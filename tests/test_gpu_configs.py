@@ -143,6 +143,30 @@ def test_config4_synthetic64_4097_band_8192spp(gpu, rnd0):
     r.close()
 
 
+def test_metric_config_cornell_1080p_1024spp(gpu, rnd0):
+    """The north star's gate on the metric's own frame: cornell.scn at 1921x1081 (bench.py's
+    cornell1080 workload) after 1024 spp.  Whole frame: counters, finiteness and pixel =
+    toInt(colors); every 32nd row plus the last (35 rows, 3 % of the frame): colours and counters
+    bit for bit against the oracle, and the per-channel L-inf < 1e-3 the north star states
+    (`device.cu:544-791`)."""
+    W, H, spp = 1921, 1081, 1024
+    r, cam, sp = _setup("cornell", W, H, gpu)
+    sid, vlp = _schedule(spp)
+    r.path_passes(sid, vlp)
+    col, cnt = r.read_radiance()
+    assert (cnt == spp).all() and np.isfinite(col).all() and (col >= 0).all()
+    _pixels_are_toint(r, col)
+    lp = oracle.light_pass(sp, rnd0, 0)
+    linf = 0.0
+    for y in list(range(0, H, 32)) + [H - 1]:
+        ocol, ocnt, _ = oracle.path_passes(sp, rnd0, cam, W, H, lp, sid, vlp, rows=(y, y + 1))
+        linf = max(linf, float(np.abs(col[y].astype(np.float64) - ocol[y].astype(np.float64)).max()))
+        _same(col[y], ocol[y], f"row {y}")
+        _same(cnt[y], ocnt[y], f"row {y} counters")
+    assert linf < 1e-3, linf
+    r.close()
+
+
 def test_north_star_linf_cornell_513_1024spp(gpu, rnd0):
     """The north star's tolerance at a real size: cornell.scn 513x513 (configs[1]'s frame) after
     1024 spp, per-channel L-inf against the CPU path over the whole frame < 1e-3 -- and in fact 0
