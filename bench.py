@@ -312,13 +312,14 @@ def scaling_breakdown(per_dev, steps, dt, render_s, reduce_s, scaling, passes_pe
     """Where a multi-GPU step's time goes, from per-device accumulators.
 
     per_dev: one dict per GPU {kernel_ms, path_ms, launches, owned_pixels, ...} over the `steps`
-    timed steps (path_ms = path kernels + the pass-stream fold, device events).  dt = the
+    timed steps (kernel_ms = the path kernels alone; path_ms = each call's span, which overlaps
+    the next call's through the pass-stream fold, so its sum can exceed the wall time).  dt = the
     max-over-ranks wall time of the timed region, render_s = its part before the frame reduce
     (max over ranks), reduce_s = the reduce (max over ranks).  For weak scaling every GPU holds
-    the per-GPU work of the one-GPU run, so the mean device's path time is the estimate of what
-    one GPU alone would take: weak_efficiency_vs_1gpu_estimate = that / dt.  Load imbalance is
-    the slowest device's path time over the mean."""
-    ps = [max(float(d["path_ms"]), 0.0) for d in per_dev]
+    the per-GPU work of the one-GPU run, so the mean device's path-kernel time is the estimate of
+    what one GPU alone would take: weak_efficiency_vs_1gpu_estimate = that / dt.  Load imbalance
+    is the slowest device's path-kernel time over the mean."""
+    ps = [max(float(d["kernel_ms"]), 0.0) for d in per_dev]
     mean_p = sum(ps) / max(len(ps), 1)
     max_p = max(ps) if ps else 0.0
     out = {"per_device": [dict(d, kernel_ms_per_step=round(d["kernel_ms"] / steps, 4),
@@ -330,8 +331,9 @@ def scaling_breakdown(per_dev, steps, dt, render_s, reduce_s, scaling, passes_pe
            "host_gap_frac": round(max(render_s - max_p / 1e3, 0.0) / dt, 5) if dt > 0 else None}
     if scaling == "weak" and dt > 0:
         out["weak_efficiency_vs_1gpu_estimate"] = round(mean_p / 1e3 / dt, 4)
-        out["weak_efficiency_note"] = ("mean device path time (one GPU's share = the one-GPU run's work) / "
-                                       "the job's wall time; 1 - it = imbalance + reduce + host gaps")
+        out["weak_efficiency_note"] = ("mean device path-kernel time (one GPU's share = the one-GPU run's "
+                                       "work) / the job's wall time; 1 - it = imbalance + reduce + fold and "
+                                       "host gaps")
     return out
 
 

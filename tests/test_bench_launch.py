@@ -72,12 +72,12 @@ def test_pmc_records_cover_both_auto_outcomes_of_the_headline():
 def test_scaling_breakdown_fields():
     """a multi-GPU line says where the time goes -- per-device kernel/path ms and
     owned samples, the reduce apart from the render, imbalance and the weak-efficiency estimate."""
-    per_dev = [{"device": 0, "kernel_ms": 600.0, "path_ms": 640.0, "launches": 20, "owned_pixels": 1000},
-               {"device": 1, "kernel_ms": 660.0, "path_ms": 700.0, "launches": 20, "owned_pixels": 1000}]
+    per_dev = [{"device": 0, "kernel_ms": 640.0, "path_ms": 660.0, "launches": 20, "owned_pixels": 1000},
+               {"device": 1, "kernel_ms": 700.0, "path_ms": 720.0, "launches": 20, "owned_pixels": 1000}]
     s = bench.scaling_breakdown(per_dev, steps=20, dt=0.75, render_s=0.72, reduce_s=0.03, scaling="weak",
                                 passes_per_step=256)
-    assert [d["path_ms_per_step"] for d in s["per_device"]] == [32.0, 35.0]
-    assert [d["kernel_ms_per_step"] for d in s["per_device"]] == [30.0, 33.0]
+    assert [d["kernel_ms_per_step"] for d in s["per_device"]] == [32.0, 35.0]
+    assert [d["path_ms_per_step"] for d in s["per_device"]] == [33.0, 36.0]
     assert s["per_device"][1]["samples_per_step"] == 256000
     assert s["reduce_s"] == 0.03 and s["reduce_frac"] == 0.04
     assert abs(s["imbalance_max_over_mean"] - 700 / 670) < 1e-4
