@@ -336,6 +336,10 @@ __device__ __forceinline__ f3 cosine_tail(f3 w, f3 u, float u_phi, float u_r2, f
 #ifndef BDPT_RNG_PAIR
 #define BDPT_RNG_PAIR 1
 #endif
+// paired loads: the odd-depth copy of the paired randoms at the point of use (see the loop)
+#ifndef BDPT_PAIR_AT_USE
+#define BDPT_PAIR_AT_USE 1
+#endif
 // camera terms: per-lane fp64 base in LDS, kz products formed once per workgroup
 #ifndef BDPT_CAMB
 #define BDPT_CAMB 1
@@ -519,6 +523,21 @@ __device__ __forceinline__ void load_rand5(const float* __restrict__ rnd, unsign
     q0 = rnd[j]; q1 = rnd[j + 1]; q2 = rnd[j + 2]; q3 = rnd[j + 3]; q4 = rnd[j + 4];
 #endif
 }
+
+// The same five entries through a buffer descriptor with one 32-bit offset register (the fused
+// kernel, BDPT_RNG_BUF): no 64-bit address temporaries, which the register allocator otherwise
+// took from registers a pending load writes -- and then waited for that load right after issuing it.
+__device__ __forceinline__ void load_rand5b(__amdgpu_buffer_rsrc_t rs, unsigned j, float& q0,
+                                            float& q1, float& q2, float& q3, float& q4) {
+    typedef unsigned u4v __attribute__((ext_vector_type(4)));
+    const unsigned vo = j * 4u;
+    const u4v v = __builtin_amdgcn_raw_buffer_load_b128(rs, vo, 0, 0);
+    q0 = __uint_as_float(v.x); q1 = __uint_as_float(v.y); q2 = __uint_as_float(v.z); q3 = __uint_as_float(v.w);
+    q4 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, vo, 16, 0));
+}
+#ifndef BDPT_RNG_BUF
+#define BDPT_RNG_BUF 1
+#endif
 
 #ifndef BDPT_RAND_PLANAR
 #define BDPT_RAND_PLANAR 1
@@ -847,18 +866,25 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
         cr0 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsl, jc * 4u, 0, 0));
         cr1 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsl, jc * 4u, 4, 0));
     };
+    // the linear table: plain loads (pass streams) or buffer loads (fused kernel, BDPT_RNG_BUF)
+    auto load_lin = [&](unsigned jj, float& a0, float& a1, float& a2, float& a3, float& a4) {
+#if BDPT_RNG_BUF && !defined(BDPT_ABL_RNG)
+        if constexpr (!STREAMS) { load_rand5b(rsl, jj, a0, a1, a2, a3, a4); return; }
+#endif
+        load_rand5(rnd, jj, a0, a1, a2, a3, a4);
+    };
     const __amdgpu_buffer_rsrc_t rsp = __builtin_amdgcn_make_buffer_rsrc(
         (void*)a.rndp, (short)0, (int)(BDPT_DEV_RANDP_PLANES * BDPT_DEV_RANDP_PL * 4u), 0x00020000);
     if (planar) load_rand5p(rsp, j, q0, q1, q2, q3, q4);
     else
 #endif
-    load_rand5(rnd, j, q0, q1, q2, q3, q4);
+    load_lin(j, q0, q1, q2, q3, q4);
     // BDPT_RNG_PAIR: n0..n4 = the next segment's randoms, loaded with q0..q4 at even depths
     constexpr bool kPair = !STREAMS && BDPT_RNG_PAIR;
     float n0 = 0.f, n1 = 0.f, n2 = 0.f, n3 = 0.f, n4 = 0.f;
     auto load_next = [&](unsigned jj) {                 // segment depth + 1: (jj + 5) mod (RAND_N - 5)
         const unsigned jn = jj + 5u < M5 ? jj + 5u : jj + 5u - M5;
-        load_rand5(rnd, jn, n0, n1, n2, n3, n4);
+        load_lin(jn, n0, n1, n2, n3, n4);
     };
     if constexpr (kPair) load_next(j);
     if constexpr (kParkPf) load_cam(j);
@@ -999,6 +1025,17 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
             done = id < 0;
         }
         BDPT_TICK(0);                 // camera ray + closest hit
+#if BDPT_PAIR_AT_USE
+        // paired loads: an odd-depth segment takes the randoms loaded with the previous one --
+        // here, after the closest hit and just before the shading uses them, not where the next
+        // loads are issued: a copy there made the compiler merge the loaded values through
+        // temporaries and wait for the loads it had just issued (s_waitcnt vmcnt(0) right after
+        // them), which cancelled the prefetch of every segment; at the top of the loop the wait
+        // would not overlap the closest hit.
+        if constexpr (kPair) {
+            if (alive && (depth & 1u)) { q0 = n0; q1 = n1; q2 = n2; q3 = n3; q4 = n4; }
+        }
+#endif
         if (alive) {
             if (!done) {
                 const float4 cm = tabC(id);
@@ -1448,7 +1485,9 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                 // loop (one LDS read and four integer ops per segment, against a spill; keeping j
                 // live and adding 5 per segment measured 1 % slower)
                 if (kPair && (depth & 1u)) {             // loaded with the previous segment's
+#if !BDPT_PAIR_AT_USE
                     q0 = n0; q1 = n1; q2 = n2; q3 = n3; q4 = n4;
+#endif
                 } else {
                 unsigned xyv = xy;
                 asm volatile("" : "+v"(xyv));
@@ -1458,9 +1497,18 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                 if (planar) load_rand5p(rsp, j, q0, q1, q2, q3, q4);
                 else
 #endif
+#if BDPT_PAIR_AT_USE
+                // the camera randoms first: the camera ray waits for them at the top of the loop,
+                // and the memory counter drains in issue order, so the segment loads issued after
+                // them may stay in flight through the camera ray and the closest hit
+                if (kParkPf && parked) load_cam(j);
+                load_lin(j, q0, q1, q2, q3, q4);
+                if (kPair) load_next(j);
+#else
                 load_rand5(rnd, j, q0, q1, q2, q3, q4);
                 if (kPair) load_next(j);
                 if (kParkPf && parked) load_cam(j);
+#endif
                 }
             }
         }
@@ -1481,7 +1529,7 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                     if (planar) load_rand5p(rsp, jr, q0, q1, q2, q3, q4);
                     else
 #endif
-                    load_rand5(rnd, jr, q0, q1, q2, q3, q4);
+                    load_lin(jr, q0, q1, q2, q3, q4);
                     if (kPair) load_next(jr);
                 }
             }
