@@ -336,6 +336,14 @@ __device__ __forceinline__ f3 cosine_tail(f3 w, f3 u, float u_phi, float u_r2, f
 #ifndef BDPT_RNG_PAIR
 #define BDPT_RNG_PAIR 1
 #endif
+// pass streams: the segment's randoms settled before the radiance stores (see the loop)
+// pass streams: parked lanes load their next pass's randoms at park time (see the loop)
+#ifndef BDPT_PARK_LOAD
+#define BDPT_PARK_LOAD 1
+#endif
+#ifndef BDPT_Q_SETTLED
+#define BDPT_Q_SETTLED 1
+#endif
 // paired loads: the odd-depth copy of the paired randoms at the point of use (see the loop)
 #ifndef BDPT_PAIR_AT_USE
 #define BDPT_PAIR_AT_USE 1
@@ -549,6 +557,7 @@ __device__ __forceinline__ void load_rand5p(__amdgpu_buffer_rsrc_t rs, unsigned 
     const unsigned qd = j / 25u, r = j - qd * 25u;
     const unsigned vo = (r * BDPT_DEV_RANDP_PL + qd) * 4u;
     constexpr unsigned P4 = BDPT_DEV_RANDP_PL * 4u;
+
     q0 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, vo, 0, 0));
     q1 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, vo, P4, 0));
     q2 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, vo, 2 * P4, 0));
@@ -857,6 +866,10 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
     const bool planar = STREAMS && (nslot == 1 || BDPT_REGEN_STREAMS) && a.rndp != nullptr;
     constexpr bool kRegen = BDPT_REGEN_K > 1 && (!STREAMS || BDPT_REGEN_STREAMS);
     constexpr bool kParkPf = kRegen && BDPT_PARK_PREFETCH && !STREAMS;
+    // pass streams: a parked lane loads its next pass's first randoms when it parks, with the
+    // other lanes' prefetch (loading them at the release instead wrote registers the continuing
+    // lanes' prefetch had just targeted, and the compiler waited for that prefetch first)
+    constexpr bool kParkLoad = kRegen && BDPT_PARK_LOAD && STREAMS;
     float cr0 = 0.f, cr1 = 0.f;                     // camera randoms of a released lane (kParkPf)
     // (read through a buffer descriptor: the compiler would otherwise merge them with the q0, q1
     // loads of the same addresses and copy them over behind a vmcnt(0))
@@ -1448,6 +1461,14 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
         }
 
         BDPT_TICK(4);                 // shadow results + contribution
+#if BDPT_Q_SETTLED
+        // pass streams: the segment's randoms are settled here, before this iteration's radiance
+        // stores.  The loads that refill their registers below then have no earlier load of the
+        // same registers to wait for -- the compiler otherwise waits for every outstanding memory
+        // operation there, the just-issued stores included (their loads completed long before:
+        // the shading used them; the wait appeared on paths that skip the shading).
+        if constexpr (STREAMS) asm volatile("" ::"v"(q0), "v"(q1), "v"(q2), "v"(q3), "v"(q4));
+#endif
         if (alive) {
             if (!done && ++depth > 6) done = true;                       // :621 7-segment cap
             if (done) {                                                  // :774-787
@@ -1480,7 +1501,7 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                     alive = false;
                 }
             }
-            if (alive || (kParkPf && parked)) {   // prefetch the next segment's randoms (:619)
+            if (alive || ((kParkPf || kParkLoad) && parked)) {   // the next segment's randoms (:619)
                 // 26 + 25 i and the pass's sid are rebuilt here rather than kept live across the
                 // loop (one LDS read and four integer ops per segment, against a spill; keeping j
                 // live and adding 5 per segment measured 1 % slower)
@@ -1497,6 +1518,7 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                 if (planar) load_rand5p(rsp, j, q0, q1, q2, q3, q4);
                 else
 #endif
+                {
 #if BDPT_PAIR_AT_USE
                 // the camera randoms first: the camera ray waits for them at the top of the loop,
                 // and the memory counter drains in issue order, so the segment loads issued after
@@ -1510,6 +1532,7 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                 if (kParkPf && parked) load_cam(j);
 #endif
                 }
+                }
             }
         }
         if constexpr (kRegen) {
@@ -1520,7 +1543,7 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                     parked = false;
                     alive = true;
                 }
-                if (!kParkPf && alive && fresh) {        // without BDPT_PARK_PREFETCH: load now
+                if (!kParkPf && !kParkLoad && alive && fresh) {   // not loaded at park time: now
                     unsigned xyv = xy;
                     asm volatile("" : "+v"(xyv));
                     const unsigned li = (xyv >> 16) * (unsigned)a.W + (xyv & 0xffffu);

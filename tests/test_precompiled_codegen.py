@@ -12,9 +12,10 @@ Recorded values and why they are acceptable:
     N = 11 spheres the SGPR file (106) overflows by 2 per extra sphere and the excess goes to VGPR
     lanes (v_writelane / v_readlane, no memory traffic).  These instances only run with
     specialisation off: by default a <= 64-sphere scene runs its hipRTC build;
-  * the BVH instance keeps its traversal state in SGPRs and moves 11 (pass streams) / 3 (fused)
-    of them to VGPR lanes in the same way (8 / 6 before round 3's grouped path regeneration and
-    paired random loads, 10 / 15 before the pass table of short calls moved into the kernel
+  * the BVH instance keeps its traversal state in SGPRs and moves 10 (pass streams) / 2 (fused)
+    of them to VGPR lanes in the same way (11 / 3 before round 4's settled pass-stream randoms
+    and buffer-descriptor table loads; 8 / 6 before round 3's grouped path regeneration and
+    paired random loads; 10 / 15 before the pass table of short calls moved into the kernel
     arguments).
 """
 import os
@@ -32,7 +33,7 @@ sys.path.insert(0, os.path.join(REPO, "tools"))
 
 def _sgpr_spills(n, streams):
     if n == -1:
-        return 11 if streams else 3
+        return 10 if streams else 2
     return 2 * (n - 10) if n > 10 else 0
 
 
