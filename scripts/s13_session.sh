@@ -9,3 +9,6 @@ for sc in cornell cornell_glass synthetic64; do
   VARIANTS="A:BDPT_JIT_FLAGS= B:BDPT_JIT_FLAGS=-DBDPT_PARK_LOAD=0,-DBDPT_Q_SETTLED=0 O:BDPT_JIT_FLAGS=-DBDPT_PARK_LOAD=0,-DBDPT_Q_SETTLED=0,-DBDPT_PAIR_AT_USE=0" \
     BENCH_ARGS="--scene $sc --steps 10" ROUNDS=2 bash scripts/ab_env.sh || exit 5
 done
+# the fused kernel's remaining table-read cost (BDPT_ABL_RNG: no table reads, changes results)
+echo "== caustic8 ablation"
+VARIANTS="A:BDPT_JIT_FLAGS= R:BDPT_JIT_FLAGS=-DBDPT_ABL_RNG" BENCH_ARGS="--workload caustic8 --steps 10" ROUNDS=2 bash scripts/ab_env.sh || exit 6
