@@ -82,7 +82,9 @@ struct bdpt_path_args {
     int tiles_per_band;             // > 0: grid rows enumerate only this shard's bands
     int streams;                    // pass streams S: lane (pixel, s) renders passes s, s+S, ...
     bdpt_dev_vec* rbuf;             // S > 1: per (pass, launched pixel) radiance, [npass][nloc]
-    int nloc;                       // launched pixels per pass = gridDim.y * BDPT_BTH * W
+    int nloc;                       // launched pixels per pass = tile-grid rows * BDPT_BTH * W
+    int pool;                       // > 1 (BDPT_POOL builds): a wave renders one pass over pool x 64
+                                    // consecutive launched pixels, restarting lanes on new pixels
     // BVH traversal (large scenes, kernel table index 17; see bdpt_bvh.cpp)
     const float4* bvh_nodes;        // 2 per node: {lo, skip}, {hi, leaf first|count<<24 or -1}
     const float4* bvh_geom;         // BVH spheres in leaf order {p, rad^2}

@@ -524,6 +524,15 @@ static int fused_max_passes() {
     return cap;
 }
 
+// Pixel pools for the pass-stream kernel (bdpt_kernels.hip BDPT_POOL): BDPT_POOL=R > 1 builds the
+// specialised pass-stream kernel with them and launches it with one pass per lane slice, each wave
+// rendering R x 64 pixels of its pass.
+static int pool_size() {
+    const char* e = getenv("BDPT_POOL");
+    const int v = e ? atoi(e) : 0;
+    return v < 2 ? 0 : (v > 64 ? 64 : v);
+}
+
 // The specialised kernel for the context's scene and pass-stream mode, compiled on first use;
 // nullptr = use the precompiled instance (reason in c->jit_err).
 static hipFunction_t jit_path_kernel_build(bdpt_ctx* c, bool streams, bool pair) {
@@ -582,6 +591,7 @@ static hipFunction_t jit_path_kernel_build(bdpt_ctx* c, bool streams, bool pair)
         std::vector<std::string> all = opts;
         if (!streams) all.push_back("-DBDPT_FUSED_WAVES=" + std::to_string(waves));
         if (!streams && !pair) all.push_back("-DBDPT_RNG_PAIR=0");
+        if (streams && pool_size() > 1) all.push_back("-DBDPT_POOL=1");
         if (const char* extra = getenv("BDPT_JIT_FLAGS")) {    // experiments: extra -D options
             std::string tok;
             for (const char* q = extra;; q++) {
@@ -638,7 +648,7 @@ static void jit_forget(bdpt_ctx* c) {                   // the scene or the spec
 // changes any of them gets a fresh build (BDPT_FUSED_MAX_PASSES is read once per process).
 static std::string jit_env_key() {
     std::string k;
-    for (const char* v : {"BDPT_JIT_FLAGS", "BDPT_JIT_WAVES", "BDPT_JIT_FUSED_WAVES", "BDPT_JIT_SCRATCH_OK"}) {
+    for (const char* v : {"BDPT_JIT_FLAGS", "BDPT_JIT_WAVES", "BDPT_JIT_FUSED_WAVES", "BDPT_JIT_SCRATCH_OK", "BDPT_POOL"}) {
         const char* e = getenv(v);
         k += e ? e : "";
         k += '\x1f';
@@ -1129,6 +1139,8 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
         quarter_ran = quarter && S >= 8;
         S = quarter_ran ? (S + 3) / 4 : (S + 1) / 2;
     }
+    const int pool = bvh ? 0 : pool_size();
+    if (pool > 1 && S > 1) S = chunk;                        // pools: one pass per lane slice
     c->last_streams = S;
     const int kidx = bvh ? 17 : (a.n <= 16 ? (int)a.n : 0);
     if (bvh) {
@@ -1228,9 +1240,20 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
         } else if (int rc = join_fold(c)) {                  // the fused kernel updates colors itself
             return rc;
         }
+        // pixel pools (a specialised pass-stream build with BDPT_POOL): waves of pool x 64 pixels
+        dim3 pgrid = grid;
+        a.pool = 0;
+        if (jf && a.streams > 1 && pool > 1) {
+            if (a.streams != a.npass)
+                return fail(c, BDPT_EINVAL, "bdpt_path_passes: pixel pools need one pass per stream (%d of %d)",
+                            a.streams, a.npass);
+            a.pool = pool;
+            const long span = 256L * pool;
+            pgrid = dim3((unsigned)((lanes + span - 1) / span), 1, a.streams);
+        }
         HIPCHK(c, hipEventRecord(cs.kev[2 * launches], c->stream));
         if (jf)
-            HIPCHK(c, hipModuleLaunchKernel(jf, grid.x, grid.y, grid.z, block.x, 1, 1, (unsigned)smem,
+            HIPCHK(c, hipModuleLaunchKernel(jf, pgrid.x, pgrid.y, pgrid.z, block.x, 1, 1, (unsigned)smem,
                                             c->stream, kargs, nullptr));
         else
             HIPCHK(c, hipLaunchKernel(kern, grid, block, kargs, smem, c->stream));

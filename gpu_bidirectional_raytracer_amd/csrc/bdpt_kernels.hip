@@ -336,13 +336,21 @@ __device__ __forceinline__ f3 cosine_tail(f3 w, f3 u, float u_phi, float u_r2, f
 #ifndef BDPT_RNG_PAIR
 #define BDPT_RNG_PAIR 1
 #endif
-// pass streams: the segment's randoms settled before the radiance stores (see the loop)
 // pass streams: parked lanes load their next pass's randoms at park time (see the loop)
 #ifndef BDPT_PARK_LOAD
 #define BDPT_PARK_LOAD 1
 #endif
+// pass streams: the segment's randoms settled before the radiance stores (see the loop)
 #ifndef BDPT_Q_SETTLED
 #define BDPT_Q_SETTLED 1
+#endif
+// Pass streams with pixel pools (built in with BDPT_POOL, used when the launch sets a.pool > 1):
+// a wave renders ONE pass over a.pool x 64 consecutive pixels of the launch's rows, and a lane
+// whose path ends takes the next pixel of the pool -- the lanes stay on one sid, so a restarted
+// group's random gathers stay adjacent in the planar copy, unlike lanes that restart on their
+// next pass (another sid each).
+#ifndef BDPT_POOL
+#define BDPT_POOL 0
 #endif
 // paired loads: the odd-depth copy of the paired randoms at the point of use (see the loop)
 #ifndef BDPT_PAIR_AT_USE
@@ -821,9 +829,29 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
     }
 #endif
     const int yoff = (bdpt_dev_tile_row(a, blockIdx.y) - (int)blockIdx.y) * BDPT_BTH;   // uniform
-    const int y = ly + yoff;
+    int y = ly + yoff;
     bool active = x < a.W && y < a.H;
     if (active && a.nshards > 1) active = ((y / a.band_rows) % a.nshards) == a.shard;
+    constexpr bool kPool = STREAMS && BDPT_POOL;
+    // pixel pools: this wave's pool is [pcur - 64, pend) of the launch's row-major pixels (local
+    // rows: grid row r of the tile grid is tile row bdpt_dev_tile_row(r)), lix = the lane's pixel
+    unsigned lix = 0, pcur = 0, pend = 0;
+    auto pool_pixel = [&](unsigned q, int& px, int& py) -> bool {
+        if (q >= pend) return false;
+        const int lr = (int)(q / (unsigned)a.W);
+        px = (int)q - lr * a.W;
+        py = bdpt_dev_tile_row(a, lr / BDPT_BTH) * BDPT_BTH + lr % BDPT_BTH;
+        if (py >= a.H) return false;
+        return a.nshards <= 1 || a.tiles_per_band > 0 || ((py / a.band_rows) % a.nshards) == a.shard;
+    };
+    if constexpr (kPool) {
+        const unsigned span = 64u * (unsigned)a.pool;
+        const unsigned pb = (blockIdx.x * 4u + (unsigned)wave) * span;
+        pend = pb + span < (unsigned)a.nloc ? pb + span : (unsigned)a.nloc;
+        pcur = pb + 64u;
+        lix = pb + (unsigned)lane;
+        active = pool_pixel(lix, x, y);
+    }
     // Pass p = s0 + k*S (slot k) is rendered iff counter0 + p < 30000 (one increment per pass).
     float4* SQ = Q + wave * kQueue * 2;
 
@@ -840,7 +868,7 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
     // unpacked where they are used, behind an empty asm the compiler cannot look through: left
     // to itself it hoists (float)x, (float)y and the 64-bit pass-stream store address out of the
     // path loop and then spills them at the 80-VGPR (6 waves/SIMD) bound.
-    const unsigned xy = ((unsigned)y << 16) | (unsigned)x;
+    unsigned xy = ((unsigned)y << 16) | (unsigned)x;
     const float* __restrict__ rnd = a.rnd;
     constexpr unsigned M5 = kRandN - 5u;
 
@@ -902,10 +930,11 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
     if constexpr (kPair) load_next(j);
     if constexpr (kParkPf) load_cam(j);
     f3 ro = mk(0.f, 0.f, 0.f), rd = ro, thr = ro, rad = ro, nl = ro;
-    bool specular = true, fresh = true, parked = false;
+    bool specular = true, fresh = true, parked = false, want = kPool && !active;
     bool alive = active && nslot > 0 && cnt0 + (unsigned)s0 < BDPT_DEV_COUNTER_CAP;
 
-    while (__builtin_amdgcn_ballot_w64(alive) != 0) {                   // wave-uniform loop
+    // (a pool lane without a pixel yet keeps the loop going: it draws one at the iteration's end)
+    while (__builtin_amdgcn_ballot_w64(alive || (kPool && want)) != 0) {   // wave-uniform loop
 #ifdef BDPT_STATS
         {
             const unsigned long long ma = __builtin_amdgcn_ballot_w64(alive);
@@ -1488,20 +1517,25 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                     r.x = rad.x; r.y = rad.y; r.z = rad.z;
                     unsigned xyv = xy;
                     asm volatile("" : "+v"(xyv));
-                    const int li = ((int)(xyv >> 16) - yoff) * a.W + (int)(xyv & 0xffffu);
+                    const int li = kPool ? (int)lix : ((int)(xyv >> 16) - yoff) * a.W + (int)(xyv & 0xffffu);
                     a.rbuf[(size_t)(s0 + k * S) * a.nloc + (size_t)li] = r;
                 }
-                k++;
                 fresh = true;
                 depth = 0;
-                const int pn = s0 + k * S;
-                alive = pn < a.npass && cnt0 + (unsigned)pn < BDPT_DEV_COUNTER_CAP;
-                if constexpr (kRegen) {
-                    parked = alive;
+                if constexpr (kPool) {                // the lane takes a pool pixel below
                     alive = false;
+                    want = true;
+                } else {
+                    k++;
+                    const int pn = s0 + k * S;
+                    alive = pn < a.npass && cnt0 + (unsigned)pn < BDPT_DEV_COUNTER_CAP;
+                    if constexpr (kRegen) {
+                        parked = alive;
+                        alive = false;
+                    }
                 }
             }
-            if (alive || ((kParkPf || kParkLoad) && parked)) {   // the next segment's randoms (:619)
+            if (!kPool && (alive || ((kParkPf || kParkLoad) && parked))) {   // next segment's randoms (:619)
                 // 26 + 25 i and the pass's sid are rebuilt here rather than kept live across the
                 // loop (one LDS read and four integer ops per segment, against a spill; keeping j
                 // live and adding 5 per segment measured 1 % slower)
@@ -1533,6 +1567,41 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
 #endif
                 }
                 }
+            }
+        }
+        if constexpr (kPool) {
+            // lanes whose path ended take the next pixels of the wave's pool, in lane order (a
+            // pixel outside the frame or the shard is passed over: the lane draws again)
+            unsigned long long mw = __builtin_amdgcn_ballot_w64(want);
+            while (mw != 0 && pcur < pend) {
+                const unsigned q = pcur + (unsigned)lane_prefix(mw);
+                pcur += (unsigned)__popcll(mw);
+                int px = 0, py = 0;
+                if (want && pool_pixel(q, px, py)) {
+                    want = false;
+                    lix = q;
+                    xy = ((unsigned)py << 16) | (unsigned)px;
+#if BDPT_CAMB
+                    camb[threadIdx.x] = make_double2((double)((float)px * a.inv_w) - a.half_w,
+                                                     (double)((float)py * a.inv_h) - a.half_h);
+#endif
+                    parked = true;
+                }
+                mw = __builtin_amdgcn_ballot_w64(want);
+            }
+            want = false;                             // the pool is used up
+            // the next segment's randoms (:619) for live lanes and the new pixels' first ones,
+            // one load group for both
+            if (alive || parked) {
+                unsigned xyv = xy;
+                asm volatile("" : "+v"(xyv));
+                const unsigned li = (xyv >> 16) * (unsigned)a.W + (xyv & 0xffffu);
+                j = (26u + li * 25u + depth * 5u + SID[0]) % M5;
+#if BDPT_RAND_PLANAR
+                if (planar) load_rand5p(rsp, j, q0, q1, q2, q3, q4);
+                else
+#endif
+                load_lin(j, q0, q1, q2, q3, q4);
             }
         }
         if constexpr (kRegen) {

@@ -1,0 +1,74 @@
+"""Pass streams with pixel pools (bdpt_kernels.hip BDPT_POOL, selected with BDPT_POOL=R): a wave
+renders one pass over R x 64 pixels and restarts lanes on new pixels.  Every pixel must still get
+exactly its passes, in pass order through the fold, so the frame is the oracle's bit for bit --
+whole frames, two calls (the counters carry over), pools larger than the frame's rows, and shards
+whose bands are whole tile rows (the grid enumerates only them) or not (pixels of other shards
+inside a pool are passed over)."""
+import os
+
+import numpy as np
+import pytest
+
+import gpu_bidirectional_raytracer_amd as g
+import oracle
+from conftest import SCENES
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def rnd0():
+    return oracle.mt607(0)
+
+
+def _oracle(name, W, H, sid, vlp, rnd0):
+    cam, sp = g.read_scene(os.path.join(SCENES, name + ".scn"))
+    g.update_camera(cam, W, H)
+    lp = oracle.light_pass(sp, rnd0, 0)
+    return oracle.path_passes(sp, rnd0, cam, W, H, lp, sid, vlp)
+
+
+def _render(name, W, H, sid, vlp, split, shard=None):
+    cam, sp = g.read_scene(os.path.join(SCENES, name + ".scn"))
+    g.update_camera(cam, W, H)
+    with g.Renderer(sp, W, H, cam, device=0) as r:
+        if shard:
+            r.set_shard(*shard)
+        r.set_streams(len(sid))
+        r.light_pass(0)
+        r.path_passes(sid[:split], vlp[:split])
+        r.path_passes(sid[split:], vlp[split:])
+        assert r.last_streams > 1 and r.last_specialized, r.specialize_status
+        col, cnt = r.read_radiance()
+        px = r.read_pixels()
+    return col, cnt, px
+
+
+@pytest.mark.parametrize("pool", [2, 4, 16])
+@pytest.mark.parametrize("name", ["cornell", "caustic", "cornell_glass", "synthetic64"])
+def test_pool_matches_oracle(gpu, rnd0, name, pool, monkeypatch):
+    monkeypatch.setenv("BDPT_POOL", str(pool))
+    W, H, npass = 47, 35, 16
+    s = g.PassScheduler()
+    s.light()
+    sid, vlp = s.next(npass)
+    col, cnt, px = _render(name, W, H, sid, vlp, 6)
+    ocol, ocnt, opx = _oracle(name, W, H, sid, vlp, rnd0)
+    assert np.array_equal(cnt, ocnt)
+    assert np.array_equal(col.view(np.uint32), ocol.view(np.uint32)), \
+        f"{name} pool {pool}: {int((col != ocol).sum())} values differ"
+    assert np.array_equal(px, opx)
+
+
+@pytest.mark.parametrize("band", [8, 5])
+def test_pool_shard_matches_oracle(gpu, rnd0, band, monkeypatch):
+    monkeypatch.setenv("BDPT_POOL", "4")
+    W, H, npass, N, rank = 83, 61, 12, 3, 1
+    s = g.PassScheduler()
+    s.light()
+    sid, vlp = s.next(npass)
+    col, cnt, px = _render("cornell", W, H, sid, vlp, 5, shard=(rank, N, band))
+    ocol, ocnt, opx = _oracle("cornell", W, H, sid, vlp, rnd0)
+    owned = (np.arange(H) // band) % N == rank
+    assert (cnt[owned] == npass).all() and (cnt[~owned] == 0).all() and (col[~owned] == 0).all()
+    assert np.array_equal(col[owned].view(np.uint32), ocol[owned].view(np.uint32))
