@@ -83,8 +83,9 @@ struct bdpt_path_args {
     int streams;                    // pass streams S: lane (pixel, s) renders passes s, s+S, ...
     bdpt_dev_vec* rbuf;             // S > 1: per (pass, launched pixel) radiance, [npass][nloc]
     int nloc;                       // launched pixels per pass = tile-grid rows * BDPT_BTH * W
-    int pool;                       // > 1 (BDPT_POOL builds): a wave renders one pass over pool x 64
-                                    // consecutive launched pixels, restarting lanes on new pixels
+    int pool;                       // > 0 (BDPT_POOL builds): a wave renders one pass, restarting lanes
+                                    // on new pixels, claimed in chunks of pool x 64 launched pixels
+    unsigned* pool_ctr;             // per pass of the launch: pixels claimed (zeroed per launch)
     // BVH traversal (large scenes, kernel table index 17; see bdpt_bvh.cpp)
     const float4* bvh_nodes;        // 2 per node: {lo, skip}, {hi, leaf first|count<<24 or -1}
     const float4* bvh_geom;         // BVH spheres in leaf order {p, rad^2}

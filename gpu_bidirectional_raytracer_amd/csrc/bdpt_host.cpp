@@ -122,6 +122,7 @@ struct bdpt_ctx {
     bool last_bvh = false;              // the last path-pass launch traversed the BVH
     int cus = 256;                      // compute units (auto stream count)
     bdpt_dev_vec* d_rbuf = nullptr;     // pass-stream radiance, 2 halves of rbuf_cap: [npass][nloc]
+    unsigned* d_poolctr = nullptr;      // pixel pools: claimed pixels per pass of a launch (128)
     int traversal = BDPT_TRAVERSE_AUTO; // bdpt_set_traversal
     bool has_bvh = false;               // the scene has a BVH (bdpt_bvh.cpp)
     int bvh_nn = 0, bvh_ns = 0, big_n = 0;
@@ -296,7 +297,7 @@ static int upload_scene(bdpt_ctx* c) {
 
 static void release(bdpt_ctx* c) {
     void* bufs[] = {c->d_params, c->d_rand, c->d_rndp, c->d_lp, c->d_sph, c->d_lights, c->d_geom, c->d_lightrec, c->d_colors,
-                    c->d_counter, c->d_pixels, c->d_thr, c->d_pass, c->d_rbuf, c->d_bvh_nodes,
+                    c->d_counter, c->d_pixels, c->d_thr, c->d_pass, c->d_rbuf, c->d_poolctr, c->d_bvh_nodes,
                     c->d_bvh_geom, c->d_big_geom, c->d_mat, c->d_bvh_ids, c->d_big_ids,
                     c->d_fcolors, c->d_fcounter, c->d_fpixels, c->d_ftmp, c->d_ftmpc};
     for (void* b : bufs)
@@ -524,13 +525,19 @@ static int fused_max_passes() {
     return cap;
 }
 
-// Pixel pools for the pass-stream kernel (bdpt_kernels.hip BDPT_POOL): BDPT_POOL=R > 1 builds the
-// specialised pass-stream kernel with them and launches it with one pass per lane slice, each wave
-// rendering R x 64 pixels of its pass.
+// Pixel pools for the pass-stream kernel (bdpt_kernels.hip BDPT_POOL): BDPT_POOL=R > 0 builds the
+// specialised pass-stream kernel with them and launches it with one pass per lane slice, waves
+// claiming chunks of R x 64 pixels of their pass; BDPT_POOL_GRID=G sizes the grid at G x 64
+// pixels per wave and pass.
 static int pool_size() {
     const char* e = getenv("BDPT_POOL");
     const int v = e ? atoi(e) : 0;
-    return v < 2 ? 0 : (v > 64 ? 64 : v);
+    return v < 1 ? 0 : (v > 64 ? 64 : v);
+}
+static int pool_grid() {
+    const char* e = getenv("BDPT_POOL_GRID");
+    const int v = e ? atoi(e) : 16;
+    return v < 1 ? 1 : (v > 256 ? 256 : v);
 }
 
 // The specialised kernel for the context's scene and pass-stream mode, compiled on first use;
@@ -591,7 +598,7 @@ static hipFunction_t jit_path_kernel_build(bdpt_ctx* c, bool streams, bool pair)
         std::vector<std::string> all = opts;
         if (!streams) all.push_back("-DBDPT_FUSED_WAVES=" + std::to_string(waves));
         if (!streams && !pair) all.push_back("-DBDPT_RNG_PAIR=0");
-        if (streams && pool_size() > 1) all.push_back("-DBDPT_POOL=1");
+        if (streams && pool_size() > 0) all.push_back("-DBDPT_POOL=1");
         if (const char* extra = getenv("BDPT_JIT_FLAGS")) {    // experiments: extra -D options
             std::string tok;
             for (const char* q = extra;; q++) {
@@ -647,8 +654,8 @@ static void jit_forget(bdpt_ctx* c) {                   // the scene or the spec
 // Every environment input of jit_path_kernel_build, as one memo key: an in-process A/B that
 // changes any of them gets a fresh build (BDPT_FUSED_MAX_PASSES is read once per process).
 static std::string jit_env_key() {
-    std::string k;
-    for (const char* v : {"BDPT_JIT_FLAGS", "BDPT_JIT_WAVES", "BDPT_JIT_FUSED_WAVES", "BDPT_JIT_SCRATCH_OK", "BDPT_POOL"}) {
+    std::string k = pool_size() > 0 ? "pool\x1f" : "\x1f";
+    for (const char* v : {"BDPT_JIT_FLAGS", "BDPT_JIT_WAVES", "BDPT_JIT_FUSED_WAVES", "BDPT_JIT_SCRATCH_OK"}) {
         const char* e = getenv(v);
         k += e ? e : "";
         k += '\x1f';
@@ -1140,7 +1147,7 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
         S = quarter_ran ? (S + 3) / 4 : (S + 1) / 2;
     }
     const int pool = bvh ? 0 : pool_size();
-    if (pool > 1 && S > 1) S = chunk;                        // pools: one pass per lane slice
+    if (pool > 0 && S > 1) S = chunk;                        // pools: one pass per lane slice
     c->last_streams = S;
     const int kidx = bvh ? 17 : (a.n <= 16 ? (int)a.n : 0);
     if (bvh) {
@@ -1243,12 +1250,16 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
         // pixel pools (a specialised pass-stream build with BDPT_POOL): waves of pool x 64 pixels
         dim3 pgrid = grid;
         a.pool = 0;
-        if (jf && a.streams > 1 && pool > 1) {
-            if (a.streams != a.npass)
+        a.pool_ctr = nullptr;
+        if (jf && a.streams > 1 && pool > 0) {
+            if (a.streams != a.npass || a.npass > 128)
                 return fail(c, BDPT_EINVAL, "bdpt_path_passes: pixel pools need one pass per stream (%d of %d)",
                             a.streams, a.npass);
+            if (!c->d_poolctr) HIPCHK(c, hipMalloc(&c->d_poolctr, 128 * sizeof(unsigned)));
+            HIPCHK(c, hipMemsetAsync(c->d_poolctr, 0, sizeof(unsigned) * a.npass, c->stream));
             a.pool = pool;
-            const long span = 256L * pool;
+            a.pool_ctr = c->d_poolctr;
+            const long span = 256L * pool_grid();
             pgrid = dim3((unsigned)((lanes + span - 1) / span), 1, a.streams);
         }
         HIPCHK(c, hipEventRecord(cs.kev[2 * launches], c->stream));

@@ -344,11 +344,13 @@ __device__ __forceinline__ f3 cosine_tail(f3 w, f3 u, float u_phi, float u_r2, f
 #ifndef BDPT_Q_SETTLED
 #define BDPT_Q_SETTLED 1
 #endif
-// Pass streams with pixel pools (built in with BDPT_POOL, used when the launch sets a.pool > 1):
-// a wave renders ONE pass over a.pool x 64 consecutive pixels of the launch's rows, and a lane
-// whose path ends takes the next pixel of the pool -- the lanes stay on one sid, so a restarted
-// group's random gathers stay adjacent in the planar copy, unlike lanes that restart on their
-// next pass (another sid each).
+// Pass streams with pixel pools (built in with BDPT_POOL, used when the launch sets a.pool > 0):
+// a wave renders ONE pass, and a lane whose path ends takes the next pixel of the wave's pool --
+// the lanes stay on one sid, so a restarted group's random gathers stay adjacent in the planar
+// copy, unlike lanes that restart on their next pass (another sid each).  The pools are chunks
+// of a.pool x 64 consecutive pixels of the launch's rows, claimed from the pass's counter
+// (a.pool_ctr[pass], one vector atomic per chunk) until the pass's pixels are used up, so the
+// waves of a pass finish together instead of each waiting on its own last paths.
 #ifndef BDPT_POOL
 #define BDPT_POOL 0
 #endif
@@ -833,9 +835,21 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
     bool active = x < a.W && y < a.H;
     if (active && a.nshards > 1) active = ((y / a.band_rows) % a.nshards) == a.shard;
     constexpr bool kPool = STREAMS && BDPT_POOL;
-    // pixel pools: this wave's pool is [pcur - 64, pend) of the launch's row-major pixels (local
-    // rows: grid row r of the tile grid is tile row bdpt_dev_tile_row(r)), lix = the lane's pixel
+    // pixel pools: this wave's chunk is [.., pend) of the launch's row-major pixels (local rows:
+    // grid row r of the tile grid is tile row bdpt_dev_tile_row(r)), pcur its next unused pixel,
+    // lix = the lane's pixel
     unsigned lix = 0, pcur = 0, pend = 0;
+    bool drained = false;                              // the pass's pixels are all claimed
+    auto claim = [&]() -> unsigned {                   // the next chunk of this wave's pass (uniform)
+        const unsigned span = 64u * (unsigned)a.pool;
+        unsigned b = 0;
+        if (lane == 0) b = atomicAdd(a.pool_ctr + s0, span);
+        b = __builtin_amdgcn_readlane(b, 0);
+        pcur = b;
+        pend = b + span < (unsigned)a.nloc ? b + span : (unsigned)a.nloc;
+        drained = b >= (unsigned)a.nloc;
+        return b;
+    };
     auto pool_pixel = [&](unsigned q, int& px, int& py) -> bool {
         if (q >= pend) return false;
         const int lr = (int)(q / (unsigned)a.W);
@@ -845,11 +859,8 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
         return a.nshards <= 1 || a.tiles_per_band > 0 || ((py / a.band_rows) % a.nshards) == a.shard;
     };
     if constexpr (kPool) {
-        const unsigned span = 64u * (unsigned)a.pool;
-        const unsigned pb = (blockIdx.x * 4u + (unsigned)wave) * span;
-        pend = pb + span < (unsigned)a.nloc ? pb + span : (unsigned)a.nloc;
-        pcur = pb + 64u;
-        lix = pb + (unsigned)lane;
+        lix = claim() + (unsigned)lane;
+        pcur += 64u;
         active = pool_pixel(lix, x, y);
     }
     // Pass p = s0 + k*S (slot k) is rendered iff counter0 + p < 30000 (one increment per pass).
@@ -1573,7 +1584,8 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
             // lanes whose path ended take the next pixels of the wave's pool, in lane order (a
             // pixel outside the frame or the shard is passed over: the lane draws again)
             unsigned long long mw = __builtin_amdgcn_ballot_w64(want);
-            while (mw != 0 && pcur < pend) {
+            while (mw != 0 && !drained) {
+                if (pcur >= pend && claim() >= (unsigned)a.nloc) break;
                 const unsigned q = pcur + (unsigned)lane_prefix(mw);
                 pcur += (unsigned)__popcll(mw);
                 int px = 0, py = 0;
@@ -1589,7 +1601,7 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                 }
                 mw = __builtin_amdgcn_ballot_w64(want);
             }
-            want = false;                             // the pool is used up
+            want = false;                             // the pass's pixels are used up
             // the next segment's randoms (:619) for live lanes and the new pixels' first ones,
             // one load group for both
             if (alive || parked) {

@@ -3,8 +3,11 @@
 For each N, the first and last rank's share of an N-way band shard (1/N of the rows; N x passes
 for weak scaling, the same passes with --strong) is rendered on one GPU with auto pass streams
 (after the auto mode's six measured calls) and with the S values asked for, and its device time
-is compared with the N = 1 step: efficiency = t(N=1) / t(rank share), over N for --strong.  The
-RCCL reduce is not included (it runs once per frame, not per step).
+is compared with the N = 1 step: efficiency = t(N=1) / t(rank share), over N for --strong, with t
+the wall time of back-to-back asynchronous calls between two synchronisations (as bench.py times its steps:
+a pass-stream call's fold overlaps the next call's path kernel); the device ms of the calls
+(path_ms, which ends with each call's fold) and of the path kernels alone (kernel_ms) are printed
+beside it.  The RCCL reduce is not included (it runs once per frame, not per step).
 
     python scripts/shard_probe.py [--scene cornell] [--passes 16] [--reps 3]
     python scripts/shard_probe.py --scene caustic --passes 128 --strong --streams 1,32
@@ -13,6 +16,7 @@ import argparse
 import json
 import os
 import sys
+import time
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
@@ -30,16 +34,20 @@ def run(sp, cam, W, H, sid, vlp, shard, nshards, band, streams, reps):
     r.light_pass(0)
     n = len(sid) // (reps + WARM)
     for k in range(WARM):                               # warm-up (the auto mode measures 6 calls)
-        r.path_passes(sid[k * n:(k + 1) * n], vlp[k * n:(k + 1) * n])
+        r.path_passes(sid[k * n:(k + 1) * n], vlp[k * n:(k + 1) * n], sync=False)
     r.synchronize()
     r.path_timing(reset=True)
+    r.kernel_timing(reset=True)
+    t0 = time.perf_counter()
     for k in range(WARM, WARM + reps):
-        r.path_passes(sid[k * n:(k + 1) * n], vlp[k * n:(k + 1) * n])
+        r.path_passes(sid[k * n:(k + 1) * n], vlp[k * n:(k + 1) * n], sync=False)
     r.synchronize()
+    wall = (time.perf_counter() - t0) * 1e3
     ms, launches = r.path_timing()
+    kms, _ = r.kernel_timing()
     S = r.last_streams
     r.close()
-    return ms / reps, S
+    return wall / reps, ms / reps, kms / reps, S
 
 
 def main():
@@ -63,15 +71,16 @@ def main():
         sid, vlp = sched.next(per * (args.reps + WARM))
         extra = [int(x) for x in args.streams.split(",") if x] if args.streams else ([] if N == 1 else [1])
         for streams in [0] + extra:
-            worst = 0.0
+            worst = wpath = wkern = 0.0
             for shard in sorted({0, N - 1}):
-                ms, S = run(sp, cam, W, H, sid, vlp, shard, N, args.band_rows, streams, args.reps)
-                worst = max(worst, ms)
+                wall, ms, kms, S = run(sp, cam, W, H, sid, vlp, shard, N, args.band_rows, streams, args.reps)
+                worst, wpath, wkern = max(worst, wall), max(wpath, ms), max(wkern, kms)
             if N == 1 and streams == 0:
                 t1 = worst
-            eff = t1 / worst / (N if args.strong else 1)
+            eff = t1 / worst / (N if args.strong else 1) if t1 else None
             print(json.dumps({"N": N, "streams_req": streams, "streams": S, "ms_per_step": round(worst, 3),
-                              "efficiency": round(eff, 4),
+                              "path_ms": round(wpath, 3), "kernel_ms": round(wkern, 3),
+                              "efficiency": round(eff, 4) if eff else None,
                               "whole_job_Msamples_s": round(W * H * per / worst / 1e3, 1)}),
                   flush=True)
 

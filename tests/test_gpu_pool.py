@@ -1,9 +1,10 @@
 """Pass streams with pixel pools (bdpt_kernels.hip BDPT_POOL, selected with BDPT_POOL=R): a wave
-renders one pass over R x 64 pixels and restarts lanes on new pixels.  Every pixel must still get
+renders one pass and restarts lanes on new pixels, claimed in chunks of R x 64 from the pass's
+counter (the grid: BDPT_POOL_GRID=G x 64 pixels per wave and pass).  Every pixel must still get
 exactly its passes, in pass order through the fold, so the frame is the oracle's bit for bit --
-whole frames, two calls (the counters carry over), pools larger than the frame's rows, and shards
-whose bands are whole tile rows (the grid enumerates only them) or not (pixels of other shards
-inside a pool are passed over)."""
+whole frames, two calls (the counters carry over), chunks larger than the frame, more waves than
+chunks (waves that find their pass drained), and shards whose bands are whole tile rows (the
+grid enumerates only them) or not (pixels of other shards inside a chunk are passed over)."""
 import os
 
 import numpy as np
@@ -44,10 +45,11 @@ def _render(name, W, H, sid, vlp, split, shard=None):
     return col, cnt, px
 
 
-@pytest.mark.parametrize("pool", [2, 4, 16])
+@pytest.mark.parametrize("pool,grid", [(1, 16), (4, 16), (16, 16), (4, 1), (2, 64)])
 @pytest.mark.parametrize("name", ["cornell", "caustic", "cornell_glass", "synthetic64"])
-def test_pool_matches_oracle(gpu, rnd0, name, pool, monkeypatch):
+def test_pool_matches_oracle(gpu, rnd0, name, pool, grid, monkeypatch):
     monkeypatch.setenv("BDPT_POOL", str(pool))
+    monkeypatch.setenv("BDPT_POOL_GRID", str(grid))
     W, H, npass = 47, 35, 16
     s = g.PassScheduler()
     s.light()
@@ -56,7 +58,7 @@ def test_pool_matches_oracle(gpu, rnd0, name, pool, monkeypatch):
     ocol, ocnt, opx = _oracle(name, W, H, sid, vlp, rnd0)
     assert np.array_equal(cnt, ocnt)
     assert np.array_equal(col.view(np.uint32), ocol.view(np.uint32)), \
-        f"{name} pool {pool}: {int((col != ocol).sum())} values differ"
+        f"{name} pool {pool} grid {grid}: {int((col != ocol).sum())} values differ"
     assert np.array_equal(px, opx)
 
 
