@@ -85,7 +85,8 @@ struct bdpt_path_args {
     int nloc;                       // launched pixels per pass = tile-grid rows * BDPT_BTH * W
     int pool;                       // > 0 (BDPT_POOL builds): a wave renders one pass, restarting lanes
                                     // on new pixels, claimed in chunks of pool x 64 launched pixels
-    unsigned* pool_ctr;             // per pass of the launch: pixels claimed (zeroed per launch)
+    unsigned* pool_ctr;             // per pass of the launch and eighth of its pixels: pixels claimed,
+                                    // one 128-B line each (zeroed per launch)
     // BVH traversal (large scenes, kernel table index 17; see bdpt_bvh.cpp)
     const float4* bvh_nodes;        // 2 per node: {lo, skip}, {hi, leaf first|count<<24 or -1}
     const float4* bvh_geom;         // BVH spheres in leaf order {p, rad^2}

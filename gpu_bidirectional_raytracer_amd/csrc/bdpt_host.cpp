@@ -122,7 +122,7 @@ struct bdpt_ctx {
     bool last_bvh = false;              // the last path-pass launch traversed the BVH
     int cus = 256;                      // compute units (auto stream count)
     bdpt_dev_vec* d_rbuf = nullptr;     // pass-stream radiance, 2 halves of rbuf_cap: [npass][nloc]
-    unsigned* d_poolctr = nullptr;      // pixel pools: claimed pixels per pass of a launch (128)
+    unsigned* d_poolctr = nullptr;      // pixel pools: claimed pixels per pass and eighth (128 x 8 lines)
     int traversal = BDPT_TRAVERSE_AUTO; // bdpt_set_traversal
     bool has_bvh = false;               // the scene has a BVH (bdpt_bvh.cpp)
     int bvh_nn = 0, bvh_ns = 0, big_n = 0;
@@ -534,6 +534,11 @@ static int pool_size() {
     const int v = e ? atoi(e) : 0;
     return v < 1 ? 0 : (v > 64 ? 64 : v);
 }
+static int pool_passes() {
+    const char* e = getenv("BDPT_POOL_PASSES");
+    const int v = e ? atoi(e) : 32;
+    return v < 2 ? 2 : (v > 128 ? 128 : v);
+}
 static int pool_grid() {
     const char* e = getenv("BDPT_POOL_GRID");
     const int v = e ? atoi(e) : 16;
@@ -621,7 +626,7 @@ static hipFunction_t jit_path_kernel_build(bdpt_ctx* c, bool streams, bool pair)
         int stat = 0;
         if (!coarse && !user_coarse &&
             hipFuncGetAttribute(&stat, HIP_FUNC_ATTRIBUTE_SHARED_SIZE_BYTES, fn) == hipSuccess) {
-            const size_t slots = streams ? 1 : (size_t)fused_max_passes();
+            const size_t slots = streams ? (pool_size() > 0 ? (size_t)pool_passes() : 1) : (size_t)fused_max_passes();
             const size_t dyn = sizeof(float4) * (4 * (size_t)n + 3 * slots + 5 + 4 * 128 * 2) + sizeof(unsigned) * slots;
             const size_t lds = 160 * 1024, fine = lds / (dyn + stat), half = lds / (dyn + stat - 2048);
             if (fine < (size_t)waves && half > fine) {
@@ -1147,7 +1152,15 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
         S = quarter_ran ? (S + 3) / 4 : (S + 1) / 2;
     }
     const int pool = bvh ? 0 : pool_size();
-    if (pool > 0 && S > 1) S = chunk;                        // pools: one pass per lane slice
+    if (pool > 0 && S > 1) {
+        // pools: launches of at most pool_passes() passes (their VLPs and sids are staged in LDS)
+        if (chunk > pool_passes()) {
+            chunk = pool_passes();
+            const int nch = (npass + chunk - 1) / chunk;
+            chunk = (npass + nch - 1) / nch;
+        }
+        S = chunk;
+    }
     c->last_streams = S;
     const int kidx = bvh ? 17 : (a.n <= 16 ? (int)a.n : 0);
     if (bvh) {
@@ -1223,7 +1236,11 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
         const size_t tab = bvh ? tree + a.big_n : 4 * (size_t)a.n;
         const size_t ids = bvh ? tree_ids + a.big_n : 0;
         // S per launch: a short last chunk gets no idle stream slices
-        a.streams = S < a.npass ? S : a.npass;
+        const bool st = (S < a.npass ? S : a.npass) > 1;     // the pass-stream kernel
+        // pixel pools: the specialised pass-stream build with BDPT_POOL, as one stream over all
+        // the launch's passes (bdpt_kernels.hip BDPT_POOL)
+        const bool pooled = st && pool > 0 && jf_streams != nullptr;
+        a.streams = pooled ? 1 : (S < a.npass ? S : a.npass);
         // a workgroup stages the VLPs and sids of its own passes only (bdpt_kernels.hip nslot)
         const size_t slots = ((size_t)a.npass + a.streams - 1) / a.streams;
         size_t smem = sizeof(float4) * (tab + 3 * slots + 5 + 4 * 128 * 2)
@@ -1232,15 +1249,15 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
             smem += (size_t)atoi(pad);
         if (smem > 160 * 1024)
             return fail(c, BDPT_EINVAL, "bdpt_path_passes: scene too large for LDS (%u spheres)", a.n);
-        const void* kern = bdpt_path_kernel_table[(a.streams > 1) * 18 + kidx];
-        const hipFunction_t jf = a.streams > 1 ? jf_streams : jf_fused;
+        const void* kern = bdpt_path_kernel_table[st * 18 + kidx];
+        const hipFunction_t jf = st ? jf_streams : jf_fused;
         c->last_specialized = jf != nullptr;
-        c->last_features = BDPT_FEAT_LAST_SKIP | (bvh ? BDPT_FEAT_BVH : 0) | (a.streams > 1 ? BDPT_FEAT_STREAMS : 0) |
+        c->last_features = BDPT_FEAT_LAST_SKIP | (bvh ? BDPT_FEAT_BVH : 0) | (st ? BDPT_FEAT_STREAMS : 0) |
                            (jf ? BDPT_FEAT_SPECIALIZED | BDPT_FEAT_DET_SKIP | (c->jit_zero_exit ? BDPT_FEAT_ZERO_EXIT : 0) : 0);
         void* kargs[] = {&a};
         grid.z = a.streams;
         const int half = c->rb_next;
-        if (a.streams > 1) {
+        if (st) {
             // this half was last read by the fold of the launch before the previous one
             if (c->rb_used[half]) HIPCHK(c, hipStreamWaitEvent(c->stream, c->rb_fold_ev[half], 0));
             a.rbuf = c->d_rbuf + (size_t)half * c->rbuf_cap;
@@ -1251,16 +1268,13 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
         dim3 pgrid = grid;
         a.pool = 0;
         a.pool_ctr = nullptr;
-        if (jf && a.streams > 1 && pool > 0) {
-            if (a.streams != a.npass || a.npass > 128)
-                return fail(c, BDPT_EINVAL, "bdpt_path_passes: pixel pools need one pass per stream (%d of %d)",
-                            a.streams, a.npass);
-            if (!c->d_poolctr) HIPCHK(c, hipMalloc(&c->d_poolctr, 128 * sizeof(unsigned)));
-            HIPCHK(c, hipMemsetAsync(c->d_poolctr, 0, sizeof(unsigned) * a.npass, c->stream));
+        if (pooled) {                                        // 8 queues, a 128-B line each
+            if (!c->d_poolctr) HIPCHK(c, hipMalloc(&c->d_poolctr, 8 * 128));
+            HIPCHK(c, hipMemsetAsync(c->d_poolctr, 0, 8 * 128, c->stream));
             a.pool = pool;
             a.pool_ctr = c->d_poolctr;
             const long span = 256L * pool_grid();
-            pgrid = dim3((unsigned)((lanes + span - 1) / span), 1, a.streams);
+            pgrid = dim3((unsigned)((lanes * a.npass + span - 1) / span), 1, 1);
         }
         HIPCHK(c, hipEventRecord(cs.kev[2 * launches], c->stream));
         if (jf)
@@ -1269,7 +1283,7 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
         else
             HIPCHK(c, hipLaunchKernel(kern, grid, block, kargs, smem, c->stream));
         HIPCHK(c, hipEventRecord(cs.kev[2 * launches + 1], c->stream));
-        if (a.streams > 1) {                                // the ordered fold, on fstream
+        if (st) {                                           // the ordered fold, on fstream
             grid.z = 1;
             HIPCHK(c, hipEventRecord(c->rb_path_ev[half], c->stream));
             HIPCHK(c, hipStreamWaitEvent(c->fstream, c->rb_path_ev[half], 0));

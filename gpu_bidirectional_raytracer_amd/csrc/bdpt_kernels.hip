@@ -348,9 +348,12 @@ __device__ __forceinline__ f3 cosine_tail(f3 w, f3 u, float u_phi, float u_r2, f
 // a wave renders ONE pass, and a lane whose path ends takes the next pixel of the wave's pool --
 // the lanes stay on one sid, so a restarted group's random gathers stay adjacent in the planar
 // copy, unlike lanes that restart on their next pass (another sid each).  The pools are chunks
-// of a.pool x 64 consecutive pixels of the launch's rows, claimed from the pass's counter
-// (a.pool_ctr[pass], one vector atomic per chunk) until the pass's pixels are used up, so the
-// waves of a pass finish together instead of each waiting on its own last paths.
+// of a.pool x 64 consecutive pixels of the launch's rows, each of one pass, claimed with one
+// vector atomic per chunk from a queue that runs through the launch's passes in order, so every
+// wave stays busy until the launch's work is used up (a lane's pass is its slot k).  The
+// launch's pixels are split in 8 parts with a queue each (on lines of their own): a wave claims
+// from the part of its XCD first (one counter word saturates near 90 claims/us), then from the
+// others.  The launch is one pass stream (S = 1) over all its passes' slots.
 #ifndef BDPT_POOL
 #define BDPT_POOL 0
 #endif
@@ -838,17 +841,30 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
     // pixel pools: this wave's chunk is [.., pend) of the launch's row-major pixels (local rows:
     // grid row r of the tile grid is tile row bdpt_dev_tile_row(r)), pcur its next unused pixel,
     // lix = the lane's pixel
-    unsigned lix = 0, pcur = 0, pend = 0;
-    bool drained = false;                              // the pass's pixels are all claimed
-    auto claim = [&]() -> unsigned {                   // the next chunk of this wave's pass (uniform)
-        const unsigned span = 64u * (unsigned)a.pool;
-        unsigned b = 0;
-        if (lane == 0) b = atomicAdd(a.pool_ctr + s0, span);
-        b = __builtin_amdgcn_readlane(b, 0);
-        pcur = b;
-        pend = b + span < (unsigned)a.nloc ? b + span : (unsigned)a.nloc;
-        drained = b >= (unsigned)a.nloc;
-        return b;
+    unsigned lix = 0, pcur = 0, pend = 0, cpass = 0;   // cpass: the chunk's pass (slot)
+    bool drained = false;                              // every queue is used up
+    unsigned part = 0, tries = 0;                      // the queue claimed from, queues found empty
+    if constexpr (kPool) part = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 7u;   // XCC_ID
+    auto claim = [&]() -> bool {                       // the wave's next chunk (uniform)
+        const unsigned span = 64u * (unsigned)a.pool, nl = (unsigned)a.nloc;
+        while (tries < 8u) {
+            const unsigned p0 = (unsigned)(((unsigned long long)nl * part) >> 3);
+            const unsigned p1 = (unsigned)(((unsigned long long)nl * (part + 1u)) >> 3);
+            const unsigned cpp = (p1 - p0 + span - 1u) / span;        // chunks per pass in this part
+            unsigned b = 0;
+            if (lane == 0) b = atomicAdd(a.pool_ctr + part * 32u, 1u);
+            b = __builtin_amdgcn_readlane(b, 0);
+            if (cpp > 0u && b < cpp * (unsigned)a.npass) {
+                cpass = b / cpp;
+                pcur = p0 + (b - cpass * cpp) * span;
+                pend = pcur + span < p1 ? pcur + span : p1;
+                return true;
+            }
+            part = (part + 1u) & 7u;
+            tries++;
+        }
+        drained = true;
+        return false;
     };
     auto pool_pixel = [&](unsigned q, int& px, int& py) -> bool {
         if (q >= pend) return false;
@@ -859,9 +875,10 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
         return a.nshards <= 1 || a.tiles_per_band > 0 || ((py / a.band_rows) % a.nshards) == a.shard;
     };
     if constexpr (kPool) {
-        lix = claim() + (unsigned)lane;
+        active = claim();
+        lix = pcur + (unsigned)lane;
         pcur += 64u;
-        active = pool_pixel(lix, x, y);
+        if (active) active = pool_pixel(lix, x, y);
     }
     // Pass p = s0 + k*S (slot k) is rendered iff counter0 + p < 30000 (one increment per pass).
     float4* SQ = Q + wave * kQueue * 2;
@@ -893,9 +910,9 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
         cnt0 = a.counter[i];
     }
 
-    int k = 0;                        // slot: this lane renders pass s0 + k*S next
+    int k = (int)cpass;               // slot: this lane renders pass s0 + k*S next
     unsigned depth = 0;
-    unsigned j = (ibase + SID[0]) % M5;
+    unsigned j = (ibase + SID[k]) % M5;
     float q0, q1, q2, q3, q4;
 #if BDPT_RAND_PLANAR
     // one pass per lane (pass streams, S = npass): the lanes of a wave stay on one sid and depth,
@@ -942,7 +959,7 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
     if constexpr (kParkPf) load_cam(j);
     f3 ro = mk(0.f, 0.f, 0.f), rd = ro, thr = ro, rad = ro, nl = ro;
     bool specular = true, fresh = true, parked = false, want = kPool && !active;
-    bool alive = active && nslot > 0 && cnt0 + (unsigned)s0 < BDPT_DEV_COUNTER_CAP;
+    bool alive = active && nslot > 0 && cnt0 + (unsigned)(s0 + k * S) < BDPT_DEV_COUNTER_CAP;
 
     // (a pool lane without a pixel yet keeps the loop going: it draws one at the iteration's end)
     while (__builtin_amdgcn_ballot_w64(alive || (kPool && want)) != 0) {   // wave-uniform loop
@@ -1585,13 +1602,14 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
             // pixel outside the frame or the shard is passed over: the lane draws again)
             unsigned long long mw = __builtin_amdgcn_ballot_w64(want);
             while (mw != 0 && !drained) {
-                if (pcur >= pend && claim() >= (unsigned)a.nloc) break;
+                if (pcur >= pend && !claim()) break;
                 const unsigned q = pcur + (unsigned)lane_prefix(mw);
                 pcur += (unsigned)__popcll(mw);
                 int px = 0, py = 0;
                 if (want && pool_pixel(q, px, py)) {
                     want = false;
                     lix = q;
+                    k = (int)cpass;
                     xy = ((unsigned)py << 16) | (unsigned)px;
 #if BDPT_CAMB
                     camb[threadIdx.x] = make_double2((double)((float)px * a.inv_w) - a.half_w,
@@ -1608,7 +1626,7 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                 unsigned xyv = xy;
                 asm volatile("" : "+v"(xyv));
                 const unsigned li = (xyv >> 16) * (unsigned)a.W + (xyv & 0xffffu);
-                j = (26u + li * 25u + depth * 5u + SID[0]) % M5;
+                j = (26u + li * 25u + depth * 5u + SID[k]) % M5;
 #if BDPT_RAND_PLANAR
                 if (planar) load_rand5p(rsp, j, q0, q1, q2, q3, q4);
                 else
