@@ -97,32 +97,35 @@ struct bdpt_ctx {
     // without pairing and four per lane again.  The pass-stream variant kept is the one with the
     // faster of its two calls (device time per pass); the faster fused variant replaces it only if
     // it beats that by kTuneMargin (a cold first call -- clocks still ramping -- no longer decides
-    // for the fused kernel).  tune_phase 0..5: measuring; 6: all issued; 7: decided.  Reset by
-    // scene / shard / traversal / specialisation / stream-mode changes.  BDPT_STREAMS_TUNE=0: no
-    // measurement (two passes per lane).
+    // for the fused kernel).  Two more calls measure pass streams with pixel pools (specialised
+    // builds only, bdpt_kernels.hip BDPT_POOL), which replace the pass-stream variant when faster.
+    // tune_phase 0..7: measuring; 8: all issued; 9: decided.  Reset by scene / shard / traversal /
+    // specialisation / stream-mode changes.  BDPT_STREAMS_TUNE=0: no measurement (two passes per
+    // lane).
     // (5 %: open scenes gain >= 10 % from the fused kernel, closed ones lose >= 7 %; with 2 % a
     // one-call measurement once kept the fused kernel for gantz, 7 % slower, profiles/r03_s27_*.
     // Four passes per lane: cornell_glass / cornell_mirror +1.2 %, synthetic64 -2.8 % at 128-pass
     // launches, profiles/r03_s45_ab_passes_per_lane.txt -- so it is measured, not fixed.)
     static constexpr double kTuneMargin = 0.05;
-    static constexpr int kTunePhases = 6;
+    static constexpr int kTunePhases = 8;
     bool tune_enabled = true;
     int tune_phase = 0;
     bool tune_fused = false;
     bool tune_pair = true;              // the fused variant kept: paired segment loads or not
     bool tune_quarter = false;          // the pass-stream variant kept: four passes per lane
-    long long tune_call[kTunePhases] = {-1, -1, -1, -1, -1, -1};
-    double tune_ms[kTunePhases] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    bool tune_pool = false;             // the pass-stream variant kept: pixel pools
+    long long tune_call[kTunePhases] = {-1, -1, -1, -1, -1, -1, -1, -1};
+    double tune_ms[kTunePhases] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
     // whether each tuning call really ran its role's variant: four passes per lane needs launches
     // of >= 8 passes, and the unpaired fused variant exists only as a specialised (JIT) build --
     // otherwise the role repeated another role's kernel and must not decide anything
-    bool tune_real[kTunePhases] = {false, false, false, false, false, false};
-    int tune_npass[kTunePhases] = {0, 0, 0, 0, 0, 0};
+    bool tune_real[kTunePhases] = {false, false, false, false, false, false, false, false};
+    int tune_npass[kTunePhases] = {0, 0, 0, 0, 0, 0, 0, 0};
     int last_streams = 1;               // S of the last path-pass launch
     bool last_bvh = false;              // the last path-pass launch traversed the BVH
     int cus = 256;                      // compute units (auto stream count)
     bdpt_dev_vec* d_rbuf = nullptr;     // pass-stream radiance, 2 halves of rbuf_cap: [npass][nloc]
-    unsigned* d_poolctr = nullptr;      // pixel pools: claimed pixels per pass and eighth (128 x 8 lines)
+    unsigned* d_poolctr = nullptr;      // pixel pools: claimed pixels per pass and eighth, a line each
     int traversal = BDPT_TRAVERSE_AUTO; // bdpt_set_traversal
     bool has_bvh = false;               // the scene has a BVH (bdpt_bvh.cpp)
     int bvh_nn = 0, bvh_ns = 0, big_n = 0;
@@ -154,7 +157,7 @@ struct bdpt_ctx {
     char jit_err[256] = {0};            // why the last specialisation fell back (diagnostics)
     int jit_waves = 0;                  // waves/SIMD bound of the last specialised build
     bool jit_zero_exit = false;         // the last specialised build has the black-surface exit
-    // jit_path_kernel's answer per [pass streams][paired loads] for the current scene, specialise
+    // jit_path_kernel's answer per [fused / pass streams / pools][paired loads] for the current scene, specialise
     // switch and JIT environment (jit_env_key): a call then resolves its kernel without rebuilding the option
     // strings (tens of microseconds per call, which the one-pass-per-call pattern pays every call)
     struct jit_memo_t {
@@ -162,7 +165,7 @@ struct bdpt_ctx {
         hipFunction_t fn = nullptr;
         int waves = 0;
         std::string flags, err;
-    } jit_memo[2][2];
+    } jit_memo[3][2];
     int last_features = 0;              // BDPT_FEAT_* of the last path-pass launch
     unsigned rand_seed = 0;             // seed of the current MT607 table (rand_ready)
     char err[512] = {0};
@@ -525,29 +528,34 @@ static int fused_max_passes() {
     return cap;
 }
 
-// Pixel pools for the pass-stream kernel (bdpt_kernels.hip BDPT_POOL): BDPT_POOL=R > 0 builds the
-// specialised pass-stream kernel with them and launches it with one pass per lane slice, waves
-// claiming chunks of R x 64 pixels of their pass; BDPT_POOL_GRID=G sizes the grid at G x 64
-// pixels per wave and pass.
-static int pool_size() {
+// Pixel pools for the pass-stream kernel (bdpt_kernels.hip BDPT_POOL), a specialised build of
+// its own launched with one pass per lane slice: the auto stream mode measures it (tuning roles
+// 6, 7).  BDPT_POOL: unset = measured, 0 = never, R > 0 = always (streams launches), chunks of
+// R x 64 pixels; BDPT_POOL_GRID = G: G x 64 pixels per wave and pass.
+static int pool_env() {
     const char* e = getenv("BDPT_POOL");
-    const int v = e ? atoi(e) : 0;
+    if (!e || !*e) return -1;
+    const int v = atoi(e);
     return v < 1 ? 0 : (v > 64 ? 64 : v);
 }
-static int pool_passes() {
-    const char* e = getenv("BDPT_POOL_PASSES");
-    const int v = e ? atoi(e) : 32;
-    return v < 2 ? 2 : (v > 128 ? 128 : v);
-}
-static int pool_grid() {
-    const char* e = getenv("BDPT_POOL_GRID");
-    const int v = e ? atoi(e) : 16;
-    return v < 1 ? 1 : (v > 256 ? 256 : v);
+// Launch shape of a pooled launch of nloc pixels per pass: {chunk R, grid G}.  One-session probe
+// (profiles/r04_s18_*): caustic 1921 x 1081 best at G = 64, R = 16 on the whole frame; its
+// 1/8 band (260 K pixels) best at G = 16..32, R = 2..4 (fewer waves per pass fill the chip only
+// with smaller G; chunks of G/4 keep ~4 claims per wave).
+static void pool_shape(long nloc, int* R, int* G) {
+    int g = nloc >= (1L << 20) ? 64 : (nloc >= (1L << 17) ? 32 : 16);
+    if (const char* e = getenv("BDPT_POOL_GRID")) {
+        const int v = atoi(e);
+        if (v >= 1) g = v > 256 ? 256 : v;
+    }
+    const int pe = pool_env();
+    *G = g;
+    *R = pe > 0 ? pe : (g / 4 < 1 ? 1 : g / 4);
 }
 
 // The specialised kernel for the context's scene and pass-stream mode, compiled on first use;
 // nullptr = use the precompiled instance (reason in c->jit_err).
-static hipFunction_t jit_path_kernel_build(bdpt_ctx* c, bool streams, bool pair) {
+static hipFunction_t jit_path_kernel_build(bdpt_ctx* c, bool streams, bool pair, bool pool) {
     const unsigned n = (unsigned)c->spheres.size();
     if (!c->specialize || n < 1 || n > 64) return nullptr;          // kJitEmis is 64 bits
     unsigned long long emis = 0;
@@ -603,7 +611,7 @@ static hipFunction_t jit_path_kernel_build(bdpt_ctx* c, bool streams, bool pair)
         std::vector<std::string> all = opts;
         if (!streams) all.push_back("-DBDPT_FUSED_WAVES=" + std::to_string(waves));
         if (!streams && !pair) all.push_back("-DBDPT_RNG_PAIR=0");
-        if (streams && pool_size() > 0) all.push_back("-DBDPT_POOL=1");
+        if (streams && pool) all.push_back("-DBDPT_POOL=1");
         if (const char* extra = getenv("BDPT_JIT_FLAGS")) {    // experiments: extra -D options
             std::string tok;
             for (const char* q = extra;; q++) {
@@ -626,7 +634,7 @@ static hipFunction_t jit_path_kernel_build(bdpt_ctx* c, bool streams, bool pair)
         int stat = 0;
         if (!coarse && !user_coarse &&
             hipFuncGetAttribute(&stat, HIP_FUNC_ATTRIBUTE_SHARED_SIZE_BYTES, fn) == hipSuccess) {
-            const size_t slots = streams ? (pool_size() > 0 ? (size_t)pool_passes() : 1) : (size_t)fused_max_passes();
+            const size_t slots = streams ? 1 : (size_t)fused_max_passes();
             const size_t dyn = sizeof(float4) * (4 * (size_t)n + 3 * slots + 5 + 4 * 128 * 2) + sizeof(unsigned) * slots;
             const size_t lds = 160 * 1024, fine = lds / (dyn + stat), half = lds / (dyn + stat - 2048);
             if (fine < (size_t)waves && half > fine) {
@@ -659,7 +667,7 @@ static void jit_forget(bdpt_ctx* c) {                   // the scene or the spec
 // Every environment input of jit_path_kernel_build, as one memo key: an in-process A/B that
 // changes any of them gets a fresh build (BDPT_FUSED_MAX_PASSES is read once per process).
 static std::string jit_env_key() {
-    std::string k = pool_size() > 0 ? "pool\x1f" : "\x1f";
+    std::string k;
     for (const char* v : {"BDPT_JIT_FLAGS", "BDPT_JIT_WAVES", "BDPT_JIT_FUSED_WAVES", "BDPT_JIT_SCRATCH_OK"}) {
         const char* e = getenv(v);
         k += e ? e : "";
@@ -668,15 +676,15 @@ static std::string jit_env_key() {
     return k;
 }
 
-static hipFunction_t jit_path_kernel(bdpt_ctx* c, bool streams, bool pair = true) {
+static hipFunction_t jit_path_kernel(bdpt_ctx* c, bool streams, bool pair = true, bool pool = false) {
     const std::string key = jit_env_key();
-    bdpt_ctx::jit_memo_t& m = c->jit_memo[streams][pair];
+    bdpt_ctx::jit_memo_t& m = c->jit_memo[streams ? (pool ? 2 : 1) : 0][pair];
     if (m.valid && m.flags == key) {
         snprintf(c->jit_err, sizeof c->jit_err, "%s", m.err.c_str());
         if (m.fn) { c->jit_waves = m.waves; c->jit_zero_exit = m.zero_exit; }
         return m.fn;
     }
-    hipFunction_t fn = jit_path_kernel_build(c, streams, pair);
+    hipFunction_t fn = jit_path_kernel_build(c, streams, pair, streams && pool);
     m.valid = true;
     m.fn = fn;
     m.waves = c->jit_waves;
@@ -1100,11 +1108,13 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
             const double inf = std::numeric_limits<double>::infinity();
             auto per = [&](int r) { return c->tune_real[r] ? c->tune_ms[r] / c->tune_npass[r] : inf; };
             const double half = std::min(per(0), per(3)), quarter = std::min(per(2), per(5));
+            const double pooled = std::min(per(6), per(7));
             const double fp = per(1), fn = per(4);
             c->tune_pair = !(fn < fp);                       // the default unless unpaired was measured faster
             c->tune_quarter = quarter < half;
+            c->tune_pool = pooled < std::min(half, quarter);
             const double fused = c->tune_pair ? fp : fn;
-            c->tune_fused = fused * (1.0 + bdpt_ctx::kTuneMargin) < std::min(half, quarter);
+            c->tune_fused = fused * (1.0 + bdpt_ctx::kTuneMargin) < std::min(std::min(half, quarter), pooled);
             c->tune_phase = bdpt_ctx::kTunePhases + 1;
         }
         if (c->tune_phase < bdpt_ctx::kTunePhases && npass >= 2) {
@@ -1151,16 +1161,13 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
         quarter_ran = quarter && S >= 8;
         S = quarter_ran ? (S + 3) / 4 : (S + 1) / 2;
     }
-    const int pool = bvh ? 0 : pool_size();
-    if (pool > 0 && S > 1) {
-        // pools: launches of at most pool_passes() passes (their VLPs and sids are staged in LDS)
-        if (chunk > pool_passes()) {
-            chunk = pool_passes();
-            const int nch = (npass + chunk - 1) / chunk;
-            chunk = (npass + nch - 1) / nch;
-        }
-        S = chunk;
-    }
+    // pixel pools: forced by BDPT_POOL=R, or measured (tuning roles 6, 7) and kept
+    const int penv = pool_env();
+    const bool want_pool = !bvh && S > 1 && penv != 0 &&
+                           (penv > 0 || (c->streams_req == 0 &&
+                                         (tune_role >= 6 || (tune_role < 0 && c->tune_phase == bdpt_ctx::kTunePhases + 1 &&
+                                                             c->tune_pool))));
+    if (want_pool) S = chunk;                                // one pass per lane slice
     c->last_streams = S;
     const int kidx = bvh ? 17 : (a.n <= 16 ? (int)a.n : 0);
     if (bvh) {
@@ -1197,14 +1204,15 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
         cs.kev.push_back(e);
     }
     // resolve the specialised kernels (a compile on first use) before the timed region starts
-    hipFunction_t jf_streams = nullptr, jf_fused = nullptr;
-    bool any_fused = false;
+    hipFunction_t jf_streams = nullptr, jf_fused = nullptr, jf_pool = nullptr;
+    bool any_fused = false, pool_ran = false;
     for (int p0 = 0; grid_rows > 0 && p0 < npass; p0 += chunk) {
         const int np = npass - p0 < chunk ? npass - p0 : chunk;
         const bool st = (S < np ? S : np) > 1;
         any_fused |= !st;
         if (bvh) continue;
-        if (st && !jf_streams) jf_streams = jit_path_kernel(c, true);
+        if (st && want_pool && !jf_pool) jf_pool = jit_path_kernel(c, true, true, true);
+        if (st && !jf_pool && !jf_streams) jf_streams = jit_path_kernel(c, true);
         if (!st && !jf_fused) jf_fused = jit_path_kernel(c, false, pair);
     }
     // a fused launch updates colors itself: it waits for the outstanding fold, before the call's
@@ -1237,10 +1245,8 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
         const size_t ids = bvh ? tree_ids + a.big_n : 0;
         // S per launch: a short last chunk gets no idle stream slices
         const bool st = (S < a.npass ? S : a.npass) > 1;     // the pass-stream kernel
-        // pixel pools: the specialised pass-stream build with BDPT_POOL, as one stream over all
-        // the launch's passes (bdpt_kernels.hip BDPT_POOL)
-        const bool pooled = st && pool > 0 && jf_streams != nullptr;
-        a.streams = pooled ? 1 : (S < a.npass ? S : a.npass);
+        const bool pooled = st && jf_pool != nullptr;        // its pixel-pool build
+        a.streams = S < a.npass ? S : a.npass;
         // a workgroup stages the VLPs and sids of its own passes only (bdpt_kernels.hip nslot)
         const size_t slots = ((size_t)a.npass + a.streams - 1) / a.streams;
         size_t smem = sizeof(float4) * (tab + 3 * slots + 5 + 4 * 128 * 2)
@@ -1250,9 +1256,10 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
         if (smem > 160 * 1024)
             return fail(c, BDPT_EINVAL, "bdpt_path_passes: scene too large for LDS (%u spheres)", a.n);
         const void* kern = bdpt_path_kernel_table[st * 18 + kidx];
-        const hipFunction_t jf = st ? jf_streams : jf_fused;
+        const hipFunction_t jf = st ? (pooled ? jf_pool : jf_streams) : jf_fused;
         c->last_specialized = jf != nullptr;
         c->last_features = BDPT_FEAT_LAST_SKIP | (bvh ? BDPT_FEAT_BVH : 0) | (st ? BDPT_FEAT_STREAMS : 0) |
+                           (pooled ? BDPT_FEAT_POOLS : 0) |
                            (jf ? BDPT_FEAT_SPECIALIZED | BDPT_FEAT_DET_SKIP | (c->jit_zero_exit ? BDPT_FEAT_ZERO_EXIT : 0) : 0);
         void* kargs[] = {&a};
         grid.z = a.streams;
@@ -1268,13 +1275,19 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
         dim3 pgrid = grid;
         a.pool = 0;
         a.pool_ctr = nullptr;
-        if (pooled) {                                        // 8 queues, a 128-B line each
-            if (!c->d_poolctr) HIPCHK(c, hipMalloc(&c->d_poolctr, 8 * 128));
-            HIPCHK(c, hipMemsetAsync(c->d_poolctr, 0, 8 * 128, c->stream));
-            a.pool = pool;
+        if (pooled) {                                        // per pass 8 counters, a 128-B line each
+            if (a.streams != a.npass || a.npass > 128)
+                return fail(c, BDPT_EINVAL, "bdpt_path_passes: pixel pools need one pass per stream (%d of %d)",
+                            a.streams, a.npass);
+            if (!c->d_poolctr) HIPCHK(c, hipMalloc(&c->d_poolctr, 128 * 8 * 128));
+            HIPCHK(c, hipMemsetAsync(c->d_poolctr, 0, (size_t)a.npass * 8 * 128, c->stream));
+            int R = 1, G = 1;
+            pool_shape(lanes, &R, &G);
+            a.pool = R;
             a.pool_ctr = c->d_poolctr;
-            const long span = 256L * pool_grid();
-            pgrid = dim3((unsigned)((lanes * a.npass + span - 1) / span), 1, 1);
+            const long span = 256L * G;
+            pgrid = dim3((unsigned)((lanes + span - 1) / span), 1, a.streams);
+            pool_ran = true;
         }
         HIPCHK(c, hipEventRecord(cs.kev[2 * launches], c->stream));
         if (jf)
@@ -1303,6 +1316,7 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
     if (tune_role >= 0) {
         c->tune_real[tune_role] = tune_role == 2 || tune_role == 5 ? quarter_ran
                                   : tune_role == 1 || tune_role == 4 ? (jf_fused != nullptr || tune_role == 1)
+                                  : tune_role >= 6 ? pool_ran
                                   : true;
         c->tune_call[tune_role] = c->issued;
         c->tune_npass[tune_role] = npass;

@@ -348,12 +348,12 @@ __device__ __forceinline__ f3 cosine_tail(f3 w, f3 u, float u_phi, float u_r2, f
 // a wave renders ONE pass, and a lane whose path ends takes the next pixel of the wave's pool --
 // the lanes stay on one sid, so a restarted group's random gathers stay adjacent in the planar
 // copy, unlike lanes that restart on their next pass (another sid each).  The pools are chunks
-// of a.pool x 64 consecutive pixels of the launch's rows, each of one pass, claimed with one
-// vector atomic per chunk from a queue that runs through the launch's passes in order, so every
-// wave stays busy until the launch's work is used up (a lane's pass is its slot k).  The
-// launch's pixels are split in 8 parts with a queue each (on lines of their own): a wave claims
-// from the part of its XCD first (one counter word saturates near 90 claims/us), then from the
-// others.  The launch is one pass stream (S = 1) over all its passes' slots.
+// of a.pool x 64 consecutive pixels of the launch's rows, claimed with one vector atomic per
+// chunk until the pass's pixels are used up, so the waves of a pass finish together instead of
+// each waiting on its own last paths.  A pass's pixels are split in 8 parts with a counter each
+// (on lines of their own), and a wave claims from the part of its XCD first (one counter word
+// saturates near 90 claims/us), then from the others.  (A single queue running through all the
+// launch's passes, lanes carrying their pass, measured slower at one GPU: caustic8 -18 %.)
 #ifndef BDPT_POOL
 #define BDPT_POOL 0
 #endif
@@ -841,23 +841,21 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
     // pixel pools: this wave's chunk is [.., pend) of the launch's row-major pixels (local rows:
     // grid row r of the tile grid is tile row bdpt_dev_tile_row(r)), pcur its next unused pixel,
     // lix = the lane's pixel
-    unsigned lix = 0, pcur = 0, pend = 0, cpass = 0;   // cpass: the chunk's pass (slot)
-    bool drained = false;                              // every queue is used up
-    unsigned part = 0, tries = 0;                      // the queue claimed from, queues found empty
+    unsigned lix = 0, pcur = 0, pend = 0;
+    bool drained = false;                              // the pass's pixels are all claimed
+    unsigned part = 0, tries = 0;                      // the part claimed from, parts found empty
     if constexpr (kPool) part = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 7u;   // XCC_ID
-    auto claim = [&]() -> bool {                       // the wave's next chunk (uniform)
+    auto claim = [&]() -> bool {                       // the next chunk of this wave's pass (uniform)
         const unsigned span = 64u * (unsigned)a.pool, nl = (unsigned)a.nloc;
         while (tries < 8u) {
             const unsigned p0 = (unsigned)(((unsigned long long)nl * part) >> 3);
             const unsigned p1 = (unsigned)(((unsigned long long)nl * (part + 1u)) >> 3);
-            const unsigned cpp = (p1 - p0 + span - 1u) / span;        // chunks per pass in this part
             unsigned b = 0;
-            if (lane == 0) b = atomicAdd(a.pool_ctr + part * 32u, 1u);
-            b = __builtin_amdgcn_readlane(b, 0);
-            if (cpp > 0u && b < cpp * (unsigned)a.npass) {
-                cpass = b / cpp;
-                pcur = p0 + (b - cpass * cpp) * span;
-                pend = pcur + span < p1 ? pcur + span : p1;
+            if (lane == 0) b = atomicAdd(a.pool_ctr + ((unsigned)s0 * 8u + part) * 32u, span);
+            b = p0 + __builtin_amdgcn_readlane(b, 0);
+            if (b < p1) {
+                pcur = b;
+                pend = b + span < p1 ? b + span : p1;
                 return true;
             }
             part = (part + 1u) & 7u;
@@ -910,7 +908,7 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
         cnt0 = a.counter[i];
     }
 
-    int k = (int)cpass;               // slot: this lane renders pass s0 + k*S next
+    int k = 0;                        // slot: this lane renders pass s0 + k*S next
     unsigned depth = 0;
     unsigned j = (ibase + SID[k]) % M5;
     float q0, q1, q2, q3, q4;
@@ -1609,7 +1607,6 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                 if (want && pool_pixel(q, px, py)) {
                     want = false;
                     lix = q;
-                    k = (int)cpass;
                     xy = ((unsigned)py << 16) | (unsigned)px;
 #if BDPT_CAMB
                     camb[threadIdx.x] = make_double2((double)((float)px * a.inv_w) - a.half_w,

@@ -97,15 +97,16 @@ int  bdpt_set_shard(bdpt_ctx *ctx, int shard, int nshards, int band_rows);
 /* Pass streams (no reference counterpart; results are bit-identical for every S): S lanes per
  * pixel render passes s, s+S, ... into an HBM radiance buffer (12 B per pass and pixel) and an
  * ordered fold applies the running mean of device.cu:774-787 in pass order.
- *   0  = auto (default): the first six calls of >= 2 passes measure, in this order, the
+ *   0  = auto (default): the first eight calls of >= 2 passes measure, in this order, the
  *        pass-stream kernel with two passes per lane (S = ceil(passes / 2); one per lane in
  *        launches of < 4 passes or with the BVH), the fused kernel with paired segment loads,
  *        pass streams with four passes per lane (S = ceil(passes / 4), launches of >= 8), two
- *        per lane again, the fused kernel without pairing and four per lane again; later calls
- *        use the pass-stream variant with the faster of its two calls, or the faster fused
- *        variant if its device time per pass beat that by 5 % (closed scenes with long paths
- *        favour pass streams, open scenes with short paths the fused kernel); re-measured after
- *        a scene / shard / traversal change;
+ *        per lane again, the fused kernel without pairing, four per lane again, and twice pass
+ *        streams with pixel pools (S = passes, lanes restart on new pixels of their pass;
+ *        specialised builds, BDPT_FEAT_POOLS); later calls use the pass-stream variant with the
+ *        fastest call, or the faster fused variant if its device time per pass beat that by 5 %
+ *        (closed scenes with long paths favour pass streams, open scenes with short paths the
+ *        fused kernel or pools); re-measured after a scene / shard / traversal change;
  *  -1  = BDPT_STREAMS_PER_LANE: always one pass per lane (S = passes per launch, <= 128);
  *   1  = the fused kernel that keeps the running mean in registers (no buffer);
  *  2..128 = that many streams. */
@@ -142,6 +143,8 @@ int  bdpt_last_traversal(const bdpt_ctx *ctx);
 #define BDPT_FEAT_LAST_SKIP   8             /* no next direction after the 7th segment        */
 #define BDPT_FEAT_BVH        16             /* BVH traversal (large scenes)                   */
 #define BDPT_FEAT_STREAMS    32             /* pass streams (one pass per lane + ordered fold)*/
+#define BDPT_FEAT_POOLS      64             /* pass streams with pixel pools (lanes restart on
+                                               new pixels of their pass, claimed in chunks)   */
 int  bdpt_last_kernel_features(const bdpt_ctx *ctx);
 /* The black-surface exit rule (BDPT_FEAT_ZERO_EXIT): 1 if ending a path at a black non-emitter is
  * provably exact for this scene -- every term the reference adds after the black hit is finite,

@@ -2,7 +2,7 @@
 
 For each N, the first and last rank's share of an N-way band shard (1/N of the rows; N x passes
 for weak scaling, the same passes with --strong) is rendered on one GPU with auto pass streams
-(after the auto mode's six measured calls) and with the S values asked for, and its device time
+(after the auto mode's eight measured calls) and with the S values asked for, and its device time
 is compared with the N = 1 step: efficiency = t(N=1) / t(rank share), over N for --strong, with t
 the wall time of back-to-back asynchronous calls between two synchronisations (as bench.py times its steps:
 a pass-stream call's fold overlaps the next call's path kernel); the device ms of the calls
@@ -24,7 +24,7 @@ sys.path.insert(0, REPO)
 import gpu_bidirectional_raytracer_amd as g  # noqa: E402
 
 
-WARM = 7
+WARM = 9
 
 
 def run(sp, cam, W, H, sid, vlp, shard, nshards, band, streams, reps):

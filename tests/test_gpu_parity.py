@@ -204,34 +204,37 @@ def test_per_lane_streams_policy(gpu):
 
 @pytest.mark.parametrize("name", ["cornell", "caustic"])
 def test_auto_streams_measured(gpu, rnd0, name):
-    """Auto (0): the first six calls of >= 2 passes run pass streams with two passes per lane
+    """Auto (0): the first eight calls of >= 2 passes run pass streams with two passes per lane
     (launches of >= 4 passes), the fused kernel with paired segment loads, pass streams with four
-    passes per lane (launches of >= 8), two per lane again, the fused kernel without pairing and
-    four per lane again; later calls use the faster pass-stream variant, or the faster fused one
+    passes per lane (launches of >= 8), two per lane again, the fused kernel without pairing,
+    four per lane again, and twice pass streams with pixel pools (one pass per lane slice, S =
+    the call's passes); later calls use the fastest pass-stream variant, or the faster fused one
     if it measured faster still; a scene change measures again.  Every call's result is the
     oracle's whatever was chosen."""
     W, H = 97, 65
     r, cam, sp = make(name, W, H, gpu)
-    sid, vlp = schedule(80)
+    sid, vlp = schedule(96)
     r.path_passes(sid[:1], vlp[:1])                        # 1 pass: not a measurement
     assert r.last_streams == 1
-    for k, want in enumerate((4, 1, 2, 4, 1, 2)):         # the six measured calls of 8 passes
+    for k, want in enumerate((4, 1, 2, 4, 1, 2, 8, 8)):   # the eight measured calls of 8 passes
         a0 = 1 + 8 * k
         r.path_passes(sid[a0:a0 + 8], vlp[a0:a0 + 8])
         assert r.last_streams == want, (k, r.last_streams)
+        if k >= 6:
+            assert "pixel_pools" in r.last_features, (k, r.last_features)
     used = []
-    for a0 in (49, 57):
+    for a0 in (65, 73):
         r.path_passes(sid[a0:a0 + 8], vlp[a0:a0 + 8])
         used.append(r.last_streams)
-    assert used[0] == used[1] and used[0] in (1, 2, 4), used
+    assert used[0] == used[1] and used[0] in (1, 2, 4, 8), used
     col, cnt = r.read_radiance()
     lp = oracle.light_pass(sp, rnd0, 0)
-    ocol, ocnt, opix = oracle.path_passes(sp, rnd0, cam, W, H, lp, sid[:65], vlp[:65])
+    ocol, ocnt, opix = oracle.path_passes(sp, rnd0, cam, W, H, lp, sid[:81], vlp[:81])
     assert_same(cnt, ocnt, "counter")
     assert_same(col, ocol, "colors")
     assert_same(r.read_pixels(), opix, "pixels")
     r.set_scene(sp)                                        # ReInitScene: measure again
-    r.path_passes(sid[65:72], vlp[65:72])
+    r.path_passes(sid[81:88], vlp[81:88])
     assert r.last_streams == 4                             # 7 passes, two per lane
     r.close()
 
