@@ -91,17 +91,17 @@ struct bdpt_ctx {
     bool rand_ready = false;
     int shard = 0, nshards = 1, band_rows = 8;
     int streams_req = 0;                // bdpt_set_streams: 0 = auto (measured), -1 = one pass per lane
-    // auto mode: the first six calls of >= 2 passes run, in this order, the pass-stream kernels
+    // auto mode: the first eight calls of >= 2 passes run, in this order, the pass-stream kernels
     // with two passes per lane, the fused S = 1 kernel with paired segment loads (bdpt_kernels.hip
     // BDPT_RNG_PAIR), pass streams with four passes per lane, two per lane again, the fused kernel
-    // without pairing and four per lane again.  The pass-stream variant kept is the one with the
-    // faster of its two calls (device time per pass); the faster fused variant replaces it only if
-    // it beats that by kTuneMargin (a cold first call -- clocks still ramping -- no longer decides
-    // for the fused kernel).  Two more calls measure pass streams with pixel pools (specialised
-    // builds only, bdpt_kernels.hip BDPT_POOL), which replace the pass-stream variant when faster.
-    // tune_phase 0..7: measuring; 8: all issued; 9: decided.  Reset by scene / shard / traversal /
-    // specialisation / stream-mode changes.  BDPT_STREAMS_TUNE=0: no measurement (two passes per
-    // lane).
+    // without pairing, four per lane again, and twice pass streams with pixel pools (specialised
+    // builds only, bdpt_kernels.hip BDPT_POOL).  The pass-stream variant kept is the one with the
+    // fastest call; the faster fused variant replaces it only if it beats that by kTuneMargin.
+    // Calls are compared per pass by path-kernel time plus a quarter of the call's fold: the fold
+    // runs on its own stream beside the next call's kernels (fold_timing).  (A cold first call -- clocks still ramping -- no
+    // longer decides for the fused kernel.)  tune_phase 0..7: measuring; 8: all issued; 9:
+    // decided.  Reset by scene / shard / traversal / specialisation / stream-mode changes.
+    // BDPT_STREAMS_TUNE=0: no measurement (two passes per lane).
     // (5 %: open scenes gain >= 10 % from the fused kernel, closed ones lose >= 7 %; with 2 % a
     // one-call measurement once kept the fused kernel for gantz, 7 % slower, profiles/r03_s27_*.
     // Four passes per lane: cornell_glass / cornell_mirror +1.2 %, synthetic64 -2.8 % at 128-pass
@@ -715,13 +715,20 @@ static int fold_timing(bdpt_ctx* c, long long upto) {
         HIPCHK(c, hipEventElapsedTime(&ms, s.ev0, s.ev1));
         c->last_ms = ms;
         c->acc_ms += ms;
-        for (int r = 0; r < bdpt_ctx::kTunePhases; r++)
-            if (c->folded == c->tune_call[r]) c->tune_ms[r] = ms;
+        double kms = 0.0;
         for (int k = 0; k < s.launches; k++) {
             float km = 0.f;
             HIPCHK(c, hipEventElapsedTime(&km, s.kev[2 * k], s.kev[2 * k + 1]));
-            c->acc_kernel_ms += km;
+            kms += km;
         }
+        c->acc_kernel_ms += kms;
+        // the stream mode's measure: the path kernels' time plus a quarter of the rest of the
+        // call (a pass-stream call's fold runs on its own stream beside the next call's path
+        // kernels and costs about that much of its own time in back-to-back calls: caustic pools
+        // 3.79 ms kernels + 1.10 ms fold -> 4.05 ms per call, two passes per lane 4.85 + 0.84 ->
+        // 4.95, profiles/r04_s20_*)
+        for (int r = 0; r < bdpt_ctx::kTunePhases; r++)
+            if (c->folded == c->tune_call[r]) c->tune_ms[r] = kms + 0.25 * ((double)ms - kms);
         c->acc_launches += s.launches;
         s.pending = false;
     }
@@ -1167,7 +1174,7 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
                            (penv > 0 || (c->streams_req == 0 &&
                                          (tune_role >= 6 || (tune_role < 0 && c->tune_phase == bdpt_ctx::kTunePhases + 1 &&
                                                              c->tune_pool))));
-    if (want_pool) S = chunk;                                // one pass per lane slice
+    if (want_pool) S = chunk < npass ? chunk : npass;        // one pass per lane slice
     c->last_streams = S;
     const int kidx = bvh ? 17 : (a.n <= 16 ? (int)a.n : 0);
     if (bvh) {

@@ -104,7 +104,7 @@ int  bdpt_set_shard(bdpt_ctx *ctx, int shard, int nshards, int band_rows);
  *        per lane again, the fused kernel without pairing, four per lane again, and twice pass
  *        streams with pixel pools (S = passes, lanes restart on new pixels of their pass;
  *        specialised builds, BDPT_FEAT_POOLS); later calls use the pass-stream variant with the
- *        fastest call, or the faster fused variant if its device time per pass beat that by 5 %
+ *        fastest call, or the faster fused variant if its time per pass (path kernels + a quarter of the fold) beat that by 5 %
  *        (closed scenes with long paths favour pass streams, open scenes with short paths the
  *        fused kernel or pools); re-measured after a scene / shard / traversal change;
  *  -1  = BDPT_STREAMS_PER_LANE: always one pass per lane (S = passes per launch, <= 128);

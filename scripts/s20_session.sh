@@ -3,7 +3,7 @@
 # caustic8 / cornell / simple (auto vs pools disabled) and the caustic probe
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; mkdir -p gpurun_out; export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest tests/test_gpu_pool.py tests/test_gpu_parity.py tests/test_gpu_specialize.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/s20_pytest.log 2>&1
+timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/s20_pytest.log 2>&1
 rc=$?; tail -3 gpurun_out/s20_pytest.log; [ $rc -eq 0 ] || exit $rc
 for sc in "--workload caustic8" "--scene cornell" "--scene simple" "--scene open"; do
   echo "== $sc"
