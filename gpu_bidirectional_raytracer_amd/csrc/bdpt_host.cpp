@@ -1292,8 +1292,9 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
             pool_shape(lanes, &R, &G);
             a.pool = R;
             a.pool_ctr = c->d_poolctr;
-            const long span = 256L * G;
-            pgrid = dim3((unsigned)((lanes + span - 1) / span), 1, a.streams);
+            // 1-D, passes interleaved in groups of 8 workgroups (bdpt_kernels.hip s0)
+            const long span = 256L * G, per = ((lanes + span - 1) / span + 7) / 8 * 8;
+            pgrid = dim3((unsigned)(per * a.streams), 1, 1);
             pool_ran = true;
         }
         HIPCHK(c, hipEventRecord(cs.kev[2 * launches], c->stream));

@@ -693,7 +693,12 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
     // of their pixels (S == 1: all, and each lane keeps the running mean itself; S > 1: radiance
     // goes to rbuf, bdpt_accum_kernel folds it in pass order).  Only the slots' VLPs and sids are
     // staged in LDS (one pass per workgroup with the default S = npass; bdpt_host.cpp sizes it).
-    const int S = STREAMS ? a.streams : 1, s0 = STREAMS ? (int)blockIdx.z : 0;
+    constexpr bool kPool = STREAMS && BDPT_POOL;
+    // pixel pools: a 1-D grid with the passes interleaved, so every pass has workgroups from the
+    // launch's start to its end and the passes finish together (z-major, the last passes ran at
+    // the end on their own workgroups); pass (b / 8) mod S keeps each pass on all 8 XCDs
+    const int S = STREAMS ? a.streams : 1;
+    const int s0 = !STREAMS ? 0 : kPool ? (int)((blockIdx.x >> 3) % (unsigned)S) : (int)blockIdx.z;
     const int nslot = (a.npass - s0 + S - 1) / S;
     const int mslot = (a.npass + S - 1) / S;         // slots of the LDS layout (any s0)
     float4* C = smem;                 // {cx, cy, cz, bits(refl | emissive<<8)}
@@ -837,7 +842,6 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
     int y = ly + yoff;
     bool active = x < a.W && y < a.H;
     if (active && a.nshards > 1) active = ((y / a.band_rows) % a.nshards) == a.shard;
-    constexpr bool kPool = STREAMS && BDPT_POOL;
     // pixel pools: this wave's chunk is [.., pend) of the launch's row-major pixels (local rows:
     // grid row r of the tile grid is tile row bdpt_dev_tile_row(r)), pcur its next unused pixel,
     // lix = the lane's pixel

@@ -1,0 +1,10 @@
+#!/bin/bash
+# round 4 s21: pool launch shape at the caustic N = 8 share (grid G, chunk R), forced pools
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; mkdir -p gpurun_out; export TMPDIR=/tmp
+for GR in "8 2" "16 2" "16 4" "32 4" "32 8" "64 16"; do
+  set -- $GR
+  echo "== grid $1 chunk $2"
+  BDPT_POOL=$2 BDPT_POOL_GRID=$1 timeout -k 10 300 python scripts/shard_probe.py --scene caustic --passes 128 --strong --ns 8 --reps 10 --streams 128 > gpurun_out/s21_$1_$2.log 2>&1 || exit 8
+  grep '^{' gpurun_out/s21_$1_$2.log | grep '"streams_req": 128'
+done
