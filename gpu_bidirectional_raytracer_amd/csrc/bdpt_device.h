@@ -22,7 +22,7 @@
 #define BDPT_DEV_N_PER_RNG 1876
 #define BDPT_DEV_LIGHT_POINTS 4096
 #define BDPT_DEV_COUNTER_CAP 30000u
-#define BDPT_DEV_INLINE_PASSES 16       // launches of <= this many passes carry sid/vlp by value
+#define BDPT_DEV_INLINE_PASSES 128      // launches of <= this many passes carry sid/vlp by value
 #define BDPT_DEV_BVH_EMISSIVE (1 << 30)   // BVH sphere id flag (bdpt_bvh.h kBvhEmissive)
 #define BDPT_DEV_DIFF 0
 #define BDPT_DEV_SPEC 1
@@ -65,7 +65,7 @@ struct bdpt_path_args {
     const unsigned* sid;            // per pass (nullptr: the pass table is sid_inl / vlp_inl)
     const int* vlp;                 // per pass
     int npass;
-    // a launch of <= BDPT_DEV_INLINE_PASSES passes (the reference's one pass per call) carries its
+    // a launch of <= BDPT_DEV_INLINE_PASSES passes (every launch of bdpt_path_passes) carries its
     // pass table in the arguments: no upload, no copy kernel before the path kernel
     unsigned sid_inl[BDPT_DEV_INLINE_PASSES];
     int vlp_inl[BDPT_DEV_INLINE_PASSES];
@@ -86,7 +86,8 @@ struct bdpt_path_args {
     int pool;                       // > 0 (BDPT_POOL builds): a wave renders one pass, restarting lanes
                                     // on new pixels, claimed in chunks of pool x 64 launched pixels
     unsigned* pool_ctr;             // per pass of the launch and eighth of its pixels: pixels claimed,
-                                    // one 128-B line each (zeroed per launch)
+                                    // one 128-B line each (zero at the launch's start)
+    unsigned* pool_ctr_next;        // the next pooled launch's counters: this launch zeroes them
     // BVH traversal (large scenes, kernel table index 17; see bdpt_bvh.cpp)
     const float4* bvh_nodes;        // 2 per node: {lo, skip}, {hi, leaf first|count<<24 or -1}
     const float4* bvh_geom;         // BVH spheres in leaf order {p, rad^2}

@@ -65,10 +65,10 @@ struct bdpt_ctx {
     bool rb_used[2] = {false, false};
     int rb_next = 0, fold_last = 0;
     bool fold_pending = false;          // a fold was issued after the last join_fold
-    // Path-pass calls go through a ring of kRing slots, each with its own pinned staging and
-    // device copy of the pass tables (sid, vlp) and its own events, so a call never waits for
-    // the GPU except on the call issued kRing calls earlier (the reference's interactive loop
-    // issues one pass per call).  Timing is folded lazily, in call order.
+    // Path-pass calls go through a ring of kRing slots, each with its own events, so a call
+    // never waits for the GPU except on the call issued kRing calls earlier (the reference's
+    // interactive loop issues one pass per call; the pass tables travel in the kernel
+    // arguments).  Timing is folded lazily, in call order.
     static constexpr int kRing = 4;
     struct call_slot {
         hipEvent_t ev0 = nullptr, ev1 = nullptr;   // the whole call
@@ -77,8 +77,6 @@ struct bdpt_ctx {
         bool pending = false;                      // issued, not folded yet
     } ring[kRing];
     long long issued = 0, folded = 0;   // calls issued / folded into the accumulators
-    unsigned* h_pass = nullptr;         // pinned staging, kRing x (2 x pass_cap)
-    unsigned* d_pass = nullptr;         // device tables, kRing x (2 x pass_cap): sid..., vlp...
     double acc_ms = 0.0;         // accumulated device time of finished path-pass calls
     long long acc_launches = 0;
     float last_ms = 0.f;
@@ -125,7 +123,9 @@ struct bdpt_ctx {
     bool last_bvh = false;              // the last path-pass launch traversed the BVH
     int cus = 256;                      // compute units (auto stream count)
     bdpt_dev_vec* d_rbuf = nullptr;     // pass-stream radiance, 2 halves of rbuf_cap: [npass][nloc]
-    unsigned* d_poolctr = nullptr;      // pixel pools: claimed pixels per pass and eighth, a line each
+    unsigned* d_poolctr = nullptr;      // pixel pools: claimed pixels per pass and eighth, a line each,
+                                        // two sets: a pooled launch uses one and zeroes the other
+    int pool_set = 0;                   // the set the next pooled launch uses
     int traversal = BDPT_TRAVERSE_AUTO; // bdpt_set_traversal
     bool has_bvh = false;               // the scene has a BVH (bdpt_bvh.cpp)
     int bvh_nn = 0, bvh_ns = 0, big_n = 0;
@@ -147,7 +147,6 @@ struct bdpt_ctx {
     unsigned* d_counter = nullptr;
     uchar4* d_pixels = nullptr;
     float* d_thr = nullptr;
-    int pass_cap = 0;
     uint32_t h_params[4 * BDPT_MT_RNG_COUNT];
     // scene-specialised path kernels (hipRTC), by compile options; modules live until destroy
     bool specialize = true;             // bdpt_set_specialize
@@ -300,7 +299,7 @@ static int upload_scene(bdpt_ctx* c) {
 
 static void release(bdpt_ctx* c) {
     void* bufs[] = {c->d_params, c->d_rand, c->d_rndp, c->d_lp, c->d_sph, c->d_lights, c->d_geom, c->d_lightrec, c->d_colors,
-                    c->d_counter, c->d_pixels, c->d_thr, c->d_pass, c->d_rbuf, c->d_poolctr, c->d_bvh_nodes,
+                    c->d_counter, c->d_pixels, c->d_thr, c->d_rbuf, c->d_poolctr, c->d_bvh_nodes,
                     c->d_bvh_geom, c->d_big_geom, c->d_mat, c->d_bvh_ids, c->d_big_ids,
                     c->d_fcolors, c->d_fcounter, c->d_fpixels, c->d_ftmp, c->d_ftmpc};
     for (void* b : bufs)
@@ -310,7 +309,6 @@ static void release(bdpt_ctx* c) {
         if (s.ev0) (void)hipEventDestroy(s.ev0);
         if (s.ev1) (void)hipEventDestroy(s.ev1);
     }
-    if (c->h_pass) (void)hipHostFree(c->h_pass);
     for (hipModule_t m : c->jit_mods) (void)hipModuleUnload(m);
     for (int b = 0; b < 2; b++) {
         if (c->rb_path_ev[b]) (void)hipEventDestroy(c->rb_path_ev[b]);
@@ -1016,29 +1014,9 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
     // this call's ring slot was last used kRing calls ago: wait for (only) that call
     const int slot = (int)(c->issued % bdpt_ctx::kRing);
     if (int rc = fold_timing(c, c->issued - bdpt_ctx::kRing + 1)) return rc;
-    if (npass > c->pass_cap) {                              // grow every slot (drain first)
-        HIPCHK(c, hipStreamSynchronize(c->stream));
-        if (int rc = fold_timing(c)) return rc;
-        if (c->d_pass) HIPCHK(c, hipFree(c->d_pass));
-        if (c->h_pass) HIPCHK(c, hipHostFree(c->h_pass));
-        c->d_pass = nullptr; c->h_pass = nullptr;
-        const int cap = npass < 1024 ? 1024 : npass;
-        const size_t words = (size_t)bdpt_ctx::kRing * 2 * cap;
-        HIPCHK(c, hipMalloc(&c->d_pass, sizeof(unsigned) * words));
-        HIPCHK(c, hipHostMalloc(&c->h_pass, sizeof(unsigned) * words, hipHostMallocDefault));
-        c->pass_cap = cap;
-    }
-    unsigned* hs = c->h_pass + (size_t)slot * 2 * c->pass_cap;
-    unsigned* ds = c->d_pass + (size_t)slot * 2 * c->pass_cap;
-    // short calls (the reference's one pass per call) pass their table in the kernel arguments
-    const bool inl = npass <= BDPT_DEV_INLINE_PASSES;
-    if (!inl) {
-        memcpy(hs, sid, sizeof(unsigned) * npass);
-        memcpy(hs + npass, vlp, sizeof(int) * npass);
-        HIPCHK(c, hipMemcpyAsync(ds, hs, sizeof(unsigned) * 2 * npass, hipMemcpyHostToDevice, c->stream));
-    }
-    const unsigned* d_sid = ds;
-    const int* d_vlp = (const int*)(ds + npass);
+    // every launch carries its pass table (<= 128 passes: the launch cap below) in the kernel
+    // arguments: no upload, no copy kernel (and its gap) before the path kernel
+    static_assert(BDPT_DEV_INLINE_PASSES >= 128, "launches of up to 128 passes");
     bdpt_ctx::call_slot& cs = c->ring[slot];
 
     bdpt_path_args a;
@@ -1230,16 +1208,11 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
     int launches = 0;
     for (int p0 = 0; grid_rows > 0 && p0 < npass; p0 += chunk, launches++) {
         a.npass = npass - p0 < chunk ? npass - p0 : chunk;
-        if (inl) {
-            a.sid = nullptr;
-            a.vlp = nullptr;
-            for (int q = 0; q < a.npass; q++) {
-                a.sid_inl[q] = sid[p0 + q];
-                a.vlp_inl[q] = vlp[p0 + q];
-            }
-        } else {
-            a.sid = d_sid + p0;
-            a.vlp = d_vlp + p0;
+        a.sid = nullptr;
+        a.vlp = nullptr;
+        for (int q = 0; q < a.npass; q++) {
+            a.sid_inl[q] = sid[p0 + q];
+            a.vlp_inl[q] = vlp[p0 + q];
         }
         // scene tables (4 per sphere, or the BVH: 2 per node + 1 per sphere) + per-pass VLPs +
         // camera + 4 wave shadow queues (results written over maxt) + sids (+ BVH sphere ids)
@@ -1286,12 +1259,18 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
             if (a.streams != a.npass || a.npass > 128)
                 return fail(c, BDPT_EINVAL, "bdpt_path_passes: pixel pools need one pass per stream (%d of %d)",
                             a.streams, a.npass);
-            if (!c->d_poolctr) HIPCHK(c, hipMalloc(&c->d_poolctr, 128 * 8 * 128));
-            HIPCHK(c, hipMemsetAsync(c->d_poolctr, 0, (size_t)a.npass * 8 * 128, c->stream));
+            constexpr size_t kSet = 128 * 8 * 32;            // words per set
+            if (!c->d_poolctr) {
+                HIPCHK(c, hipMalloc(&c->d_poolctr, 2 * kSet * sizeof(unsigned)));
+                HIPCHK(c, hipMemsetAsync(c->d_poolctr, 0, 2 * kSet * sizeof(unsigned), c->stream));
+                c->pool_set = 0;
+            }
             int R = 1, G = 1;
             pool_shape(lanes, &R, &G);
             a.pool = R;
-            a.pool_ctr = c->d_poolctr;
+            a.pool_ctr = c->d_poolctr + (size_t)c->pool_set * kSet;
+            a.pool_ctr_next = c->d_poolctr + (size_t)(c->pool_set ^ 1) * kSet;
+            c->pool_set ^= 1;
             // 1-D, passes interleaved in groups of 8 workgroups (bdpt_kernels.hip s0)
             const long span = 256L * G, per = ((lanes + span - 1) / span + 7) / 8 * 8;
             pgrid = dim3((unsigned)(per * a.streams), 1, 1);

@@ -877,6 +877,9 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
         return a.nshards <= 1 || a.tiles_per_band > 0 || ((py / a.band_rows) % a.nshards) == a.shard;
     };
     if constexpr (kPool) {
+        // the next pooled launch's counters (the previous launch used them and has finished)
+        for (unsigned w = blockIdx.x * 256u + threadIdx.x; w < 128u * 8u; w += gridDim.x * 256u)
+            a.pool_ctr_next[w * 32u] = 0u;
         active = claim();
         lix = pcur + (unsigned)lane;
         pcur += 64u;
