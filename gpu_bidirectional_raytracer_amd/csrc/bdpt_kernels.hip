@@ -344,7 +344,7 @@ __device__ __forceinline__ f3 cosine_tail(f3 w, f3 u, float u_phi, float u_r2, f
 #ifndef BDPT_Q_SETTLED
 #define BDPT_Q_SETTLED 1
 #endif
-// Pass streams with pixel pools (built in with BDPT_POOL, used when the launch sets a.pool > 0):
+// Pass streams with pixel pools (a build with BDPT_POOL; bdpt_host.cpp launches it with a.pool = R):
 // a wave renders ONE pass, and a lane whose path ends takes the next pixel of the wave's pool --
 // the lanes stay on one sid, so a restarted group's random gathers stay adjacent in the planar
 // copy, unlike lanes that restart on their next pass (another sid each).  The pools are chunks
@@ -850,7 +850,7 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
     unsigned part = 0, tries = 0;                      // the part claimed from, parts found empty
     if constexpr (kPool) part = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 7u;   // XCC_ID
     auto claim = [&]() -> bool {                       // the next chunk of this wave's pass (uniform)
-        const unsigned span = 64u * (unsigned)a.pool, nl = (unsigned)a.nloc;
+        const unsigned span = 64u * (unsigned)(a.pool > 1 ? a.pool : 1), nl = (unsigned)a.nloc;   // >= 64: claims advance
         while (tries < 8u) {
             const unsigned p0 = (unsigned)(((unsigned long long)nl * part) >> 3);
             const unsigned p1 = (unsigned)(((unsigned long long)nl * (part + 1u)) >> 3);

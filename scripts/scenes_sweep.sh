@@ -12,6 +12,7 @@ for f in assets/scenes/*.scn; do
       > gpurun_out/scene_$s.log 2>&1 || { echo "STOP $s"; tail -5 gpurun_out/scene_$s.log; exit 1; }
   python3 -c "
 import json; d=json.loads(open('gpurun_out/scene_$s.log').read().strip().splitlines()[-1]); c=d['config']
-print('$s', round(d['value']), 'S=%d' % c['pass_streams'], c['traversal'])" >> gpurun_out/scenes.txt
+f = (d.get('roofline') or {}).get('kernel_features', [])
+print('$s', round(d['value']), 'S=%d' % c['pass_streams'], c['traversal'], 'pools' if 'pixel_pools' in f else '')" >> gpurun_out/scenes.txt
 done
 cat gpurun_out/scenes.txt
