@@ -104,6 +104,7 @@ struct bdpt_path_args {
 // Tile row of a workgroup row: identity, or the sub-th tile row of this shard's k-th band.
 __device__ __forceinline__ int bdpt_dev_tile_row(const bdpt_path_args& a, int by) {
     if (a.tiles_per_band <= 0) return by;
+    if (a.tiles_per_band == 1) return a.shard + by * a.nshards;   // 8-row bands (the default)
     const int k = by / a.tiles_per_band, sub = by - k * a.tiles_per_band;
     return (a.shard + k * a.nshards) * a.tiles_per_band + sub;
 }

@@ -357,6 +357,9 @@ __device__ __forceinline__ f3 cosine_tail(f3 w, f3 u, float u_phi, float u_r2, f
 #ifndef BDPT_POOL
 #define BDPT_POOL 0
 #endif
+#ifndef BDPT_POOL_FDIV
+#define BDPT_POOL_FDIV 1
+#endif
 // paired loads: the odd-depth copy of the paired randoms at the point of use (see the loop)
 #ifndef BDPT_PAIR_AT_USE
 #define BDPT_PAIR_AT_USE 1
@@ -870,8 +873,16 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
     };
     auto pool_pixel = [&](unsigned q, int& px, int& py) -> bool {
         if (q >= pend) return false;
+        // q / W through the fp32 reciprocal (q < 2^28, W < 2^16: the estimate is off by at most
+        // one row) and one correction, instead of an integer division
+#if BDPT_POOL_FDIV
+        int lr = (int)((float)q * __builtin_amdgcn_rcpf((float)a.W));
+        px = (int)q - lr * a.W;
+        if (px < 0) { lr--; px += a.W; } else if (px >= a.W) { lr++; px -= a.W; }
+#else
         const int lr = (int)(q / (unsigned)a.W);
         px = (int)q - lr * a.W;
+#endif
         py = bdpt_dev_tile_row(a, lr / BDPT_BTH) * BDPT_BTH + lr % BDPT_BTH;
         if (py >= a.H) return false;
         return a.nshards <= 1 || a.tiles_per_band > 0 || ((py / a.band_rows) % a.nshards) == a.shard;

@@ -1,0 +1,14 @@
+#!/bin/bash
+# round 4 s30: pool pixel mapping by fp32 reciprocal (F) vs integer division (I); 8-row-band tile
+# rows without a division in both
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; mkdir -p gpurun_out; export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests/test_gpu_pool.py tests/test_gpu_configs.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/s30_pytest.log 2>&1
+rc=$?; tail -2 gpurun_out/s30_pytest.log; [ $rc -eq 0 ] || exit $rc
+for r in 1 2; do
+  for v in "F:" "I:-DBDPT_POOL_FDIV=0"; do
+    name=${v%%:*}; fl=${v#*:}
+    BDPT_JIT_FLAGS=$fl timeout -k 10 300 python scripts/shard_probe.py --scene caustic --passes 128 --strong --ns 1,8 --reps 10 > gpurun_out/s30_$name.log 2>&1 || exit 7
+    echo "round $r $name"; grep '^{' gpurun_out/s30_$name.log | grep '"streams_req": 0'
+  done
+done
