@@ -34,6 +34,15 @@ def test_library_exports_every_declared_symbol():
     assert names == set(_lib.EXPORTED), names ^ set(_lib.EXPORTED)
 
 
+def test_feature_bits_match_header():
+    """The Python names of the kernel-feature bits (Renderer.last_features) are the header's
+    BDPT_FEAT_* values, one for one."""
+    src = open(HEADER).read()
+    bits = {int(v): n for n, v in re.findall(r"#define\s+BDPT_FEAT_([A-Z_]+)\s+(\d+)", src)}
+    assert sorted(bits) == sorted(_lib.FEATURES), (bits, _lib.FEATURES)
+    assert bits[64] == "POOLS" and _lib.FEATURES[64] == "pixel_pools"
+
+
 def test_struct_layouts_match_reference_headers():
     assert ctypes.sizeof(g.Vec) == 12          # vec.h:4-6
     assert ctypes.sizeof(_lib.Sphere) == 44    # geom.h:23-27 (enum as int)
