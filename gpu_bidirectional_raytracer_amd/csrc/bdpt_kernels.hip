@@ -353,7 +353,7 @@ __device__ __forceinline__ f3 cosine_tail(f3 w, f3 u, float u_phi, float u_r2, f
 // each waiting on its own last paths.  A pass's pixels are split in 8 parts with a counter each
 // (on lines of their own), and a wave claims from the part of its XCD first (one counter word
 // saturates near 90 claims/us), then from the others.  (A single queue running through all the
-// launch's passes, lanes carrying their pass, measured slower at one GPU: caustic8 -18 %.)
+// launch's passes, lanes carrying their pass, measured slower at one GPU: caustic >= 16 %.)
 #ifndef BDPT_POOL
 #define BDPT_POOL 0
 #endif
