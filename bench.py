@@ -169,6 +169,16 @@ def resolve_launch(gpus, env, visible=None, fixed_bands=0, devices=None):
     return "inproc", 1, 0, 0
 
 
+def is_reduce_fallback(mode, devices, backend, rehearse):
+    """True when a multi-GPU frame is assembled by anything but RCCL across distinct GPUs: an
+    in-process group on distinct devices whose backend is not "rccl" (RCCL missing or
+    ncclCommInitAll failed), or torchrun ranks rehearsing over gloo.  Repeated devices (--devices
+    0,0, shards of one GPU) are a rehearsal whose peer copies are expected, not a fallback."""
+    if mode == "inproc":
+        return len(set(devices)) == len(devices) and len(devices) > 1 and backend != "rccl"
+    return bool(mode == "ranks" and rehearse)
+
+
 def _read(path):
     try:
         with open(path) as f:
@@ -364,6 +374,8 @@ def main():
                     help="multi-rank dry run on fewer GPUs: gloo, ranks share devices (not a measurement)")
     ap.add_argument("--devices", default=None,
                     help="in-process multi-device run on these devices, e.g. 0,0 (rehearsal of --gpus 2 on one GPU)")
+    ap.add_argument("--allow-peer-reduce", action="store_true",
+                    help="in-process run on distinct GPUs: time the peer-copy frame reduce if RCCL is unavailable")
     ap.add_argument("--cpu-probe", default=None, help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.cpu_probe:                                        # child of cpu_baseline: no GPU
@@ -412,7 +424,9 @@ def main():
     # bdpt_set_streams): untimed extra steps when --warmup is shorter, so the timed steps run the
     # kernel it settled on
     tune = max(0, 9 - args.warmup) if args.streams == 0 else 0
-    untimed = tune + args.warmup
+    # torchrun ranks: one more untimed step after every rank has taken rank 0's choice
+    follow = 1 if (args.streams == 0 and world > 1) else 0
+    untimed = tune + args.warmup + follow
     sid, vlp = sched.next(per_step * (untimed + args.steps))
 
     # The CPU baseline (rank 0 at N = 1) runs first, before the GPU is touched: the GPU phase
@@ -442,6 +456,11 @@ def main():
         # device k of the group renders shard k of nshards (bdpt_set_shard on a group of ndev
         # devices as shard 0 of nshards / ndev groups)
         r.set_shard(0, nshards // ndev, band)
+        # distinct GPUs must assemble the frame over RCCL: a silent peer-copy fallback (e.g. a
+        # failed ncclCommInitAll) would time another collective than the one the line names
+        if is_reduce_fallback(mode, devices, r.reduce_backend, False) and not args.allow_peer_reduce:
+            raise SystemExit(f"bench.py: the {ndev}-GPU frame reduce fell back to '{r.reduce_backend}' "
+                             "(RCCL unavailable or ncclCommInitAll failed); --allow-peer-reduce to time it anyway")
     else:
         devices = [local]
         r = g.Renderer(sp, W, H, cam, device=local)
@@ -475,9 +494,24 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    for k in range(untimed):
+    for k in range(untimed - follow):
         step(k)
     r.synchronize()
+    choice_src = None
+    if follow:
+        # every rank measured the stream-mode candidates on the same calls; rank 0's decision is
+        # the job's (the ranks run the same kernels whatever their own timings said)
+        ch = [r.stream_choice if rank == 0 else 0]
+        dist.broadcast_object_list(ch, src=0)
+        if not ch[0]:
+            raise SystemExit("bench.py: rank 0's auto stream mode has not decided after the tuning steps")
+        r.set_stream_choice(ch[0])
+        choice_src = "rank 0 (torch.distributed broadcast, applied with bdpt_set_stream_choice)"
+        for k in range(untimed - follow, untimed):
+            step(k)
+        r.synchronize()
+    elif mode == "inproc" and args.streams == 0:
+        choice_src = "devices[0] (the group's peers follow its measurement)"
     if mode == "inproc":                                      # RCCL's first-use set-up, untimed
         r.reduce_frame()
     r.path_timing(reset=True)
@@ -517,6 +551,8 @@ def main():
     kern_ms, launches = r.kernel_timing()                     # path kernels alone
     dev_ms, _ = r.path_timing()                               # + the pass-stream fold
     per_dev = r.device_timing()                               # each device's own share (no max)
+    for k, d in enumerate(per_dev):                           # the kernel each device ran
+        d["mode"] = r.device_mode(k)
     samples = job_pixels * per_step * args.steps
     value = samples / dt / 1e6
     ident = gpu_identity(local)
@@ -624,6 +660,7 @@ def main():
             reduce_backend = r.reduce_backend + " (in-process bdpt_create_multi)"
         else:
             reduce_backend = "none"
+        reduce_fallback = is_reduce_fallback(mode, devices, r.reduce_backend, args.rehearse)
         line = {
             "metric": METRIC, "value": round(value, 2), "unit": "Msamples/s", "n_gpus": units,
             "steps": args.steps, "warmup": args.warmup, "tune_steps": tune, "ms_per_step": round(dt / args.steps * 1e3, 3),
@@ -643,6 +680,8 @@ def main():
                        "specialized": r.last_specialized},
             "rccl_ranks": world if mode == "ranks" else (ndev if r.reduce_backend == "rccl" else 0),
             "reduce_backend": reduce_backend,
+            "reduce_fallback": reduce_fallback,
+            "stream_choice_from": choice_src,
             "devices": [{"rank": q, **idents[q]} for q in range(len(idents))] if mode == "ranks"
             else [{"device": d, **idents[i]} for i, d in enumerate(devices)],
             "device_ms_per_step": round(dev_ms / args.steps, 3),

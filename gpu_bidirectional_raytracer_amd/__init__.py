@@ -17,7 +17,7 @@ from typing import Optional, Sequence, Tuple
 
 import numpy as np
 
-from ._lib import (BDPT_OK, COUNTER_CAP, DEFAULT_DAT, DIFF, FEATURES, KEY_DOWN, KEY_LEFT, KEY_PAGE_DOWN,
+from ._lib import (BDPT_OK, CHOICES, COUNTER_CAP, DEFAULT_DAT, DIFF, FEATURES, KEY_DOWN, KEY_LEFT, KEY_PAGE_DOWN,
                    KEY_PAGE_UP, KEY_RIGHT, KEY_UP, LIGHT_POINTS, LITE, RAND_N, REFR, SCENE_DIR, SPEC,
                    BdptError, Camera, LightPath, PassState, RandState, Sphere, Vec, lib)
 
@@ -222,6 +222,22 @@ class Renderer:
     @property
     def last_streams(self) -> int:
         return int(lib.bdpt_last_streams(self._h))
+
+    @property
+    def stream_choice(self) -> int:
+        """BDPT_CHOICE_* bits of the auto stream mode's decision (0 while measuring / not auto)."""
+        return int(lib.bdpt_stream_choice(self._h))
+
+    def set_stream_choice(self, choice: int) -> None:
+        """Apply a decision of the auto stream mode (e.g. rank 0's) without measuring."""
+        self._chk(lib.bdpt_set_stream_choice(self._h, int(choice)))
+
+    def device_mode(self, k: int = 0) -> dict:
+        """Device k's last kernel: {streams, features, choice} (bdpt_device_mode)."""
+        st, ft, ch = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        self._chk(lib.bdpt_device_mode(self._h, k, ctypes.byref(st), ctypes.byref(ft), ctypes.byref(ch)))
+        return {"streams": st.value, "features": [n for b, n in sorted(FEATURES.items()) if ft.value & b],
+                "choice": [n for b, n in sorted(CHOICES.items()) if ch.value & b]}
 
     def set_specialize(self, on: bool) -> None:
         """Scene-specialised kernels (run-time compiled, <= 64 spheres); results are bit-identical."""

@@ -20,6 +20,7 @@ COUNTER_CAP = 30000
 BDPT_OK, BDPT_EINVAL, BDPT_EIO, BDPT_EHIP, BDPT_ENOMEM, BDPT_ESTATE = 0, -1, -2, -3, -4, -5
 DIFF, SPEC, REFR, LITE = 0, 1, 2, 3
 KEY_UP, KEY_DOWN, KEY_LEFT, KEY_RIGHT, KEY_PAGE_UP, KEY_PAGE_DOWN = range(0x101, 0x107)
+CHOICES = {1: "decided", 2: "fused", 4: "paired", 8: "quarter", 16: "pools"}   # BDPT_CHOICE_*
 FEATURES = {1: "specialized", 2: "det_skip", 4: "zero_exit", 8: "last_skip", 16: "bvh", 32: "pass_streams",
             64: "pixel_pools"}
 
@@ -76,6 +77,10 @@ _SIGS = [
     ("bdpt_set_shard", ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     ("bdpt_set_streams", ctypes.c_int, [_P, ctypes.c_int]),
     ("bdpt_last_streams", ctypes.c_int, [_P]),
+    ("bdpt_stream_choice", ctypes.c_int, [_P]),
+    ("bdpt_set_stream_choice", ctypes.c_int, [_P, ctypes.c_int]),
+    ("bdpt_device_mode", ctypes.c_int, [_P, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+                                        ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
     ("bdpt_set_specialize", ctypes.c_int, [_P, ctypes.c_int]),
     ("bdpt_last_specialized", ctypes.c_int, [_P]),
     ("bdpt_specialize_status", ctypes.c_char_p, [_P]),

@@ -119,6 +119,9 @@ struct bdpt_ctx {
     // otherwise the role repeated another role's kernel and must not decide anything
     bool tune_real[kTunePhases] = {false, false, false, false, false, false, false, false};
     int tune_npass[kTunePhases] = {0, 0, 0, 0, 0, 0, 0, 0};
+    // multi-device groups: the peers follow the stream mode devices[0] measured (its decision is
+    // copied when they reach the decision point), so every device of a group runs the same kernels
+    bdpt_ctx* tune_leader = nullptr;
     int last_streams = 1;               // S of the last path-pass launch
     bool last_bvh = false;              // the last path-pass launch traversed the BVH
     int cus = 256;                      // compute units (auto stream count)
@@ -909,6 +912,29 @@ static int one_set_streams(bdpt_ctx* c, int streams) {
 
 int bdpt_last_streams(const bdpt_ctx* c) { return c ? c->last_streams : BDPT_EINVAL; }
 
+static int choice_of(const bdpt_ctx* c) {
+    if (c->streams_req != 0 || !c->tune_enabled || c->tune_phase != bdpt_ctx::kTunePhases + 1) return 0;
+    return BDPT_CHOICE_DECIDED | (c->tune_fused ? BDPT_CHOICE_FUSED : 0) | (c->tune_pair ? BDPT_CHOICE_PAIRED : 0) |
+           (c->tune_quarter ? BDPT_CHOICE_QUARTER : 0) | (c->tune_pool ? BDPT_CHOICE_POOLS : 0);
+}
+
+static int one_set_stream_choice(bdpt_ctx* c, int choice) {
+    if (!c) return BDPT_EINVAL;
+    if (!(choice & BDPT_CHOICE_DECIDED) || (choice & ~0x1f))
+        return fail(c, BDPT_EINVAL, "bdpt_set_stream_choice: bad choice 0x%x", choice);
+    if (c->streams_req != 0)
+        return fail(c, BDPT_ESTATE, "bdpt_set_stream_choice: the stream mode is not auto (%d)", c->streams_req);
+    c->tune_fused = (choice & BDPT_CHOICE_FUSED) != 0;
+    c->tune_pair = (choice & BDPT_CHOICE_PAIRED) != 0;
+    c->tune_quarter = (choice & BDPT_CHOICE_QUARTER) != 0;
+    c->tune_pool = (choice & BDPT_CHOICE_POOLS) != 0;
+    c->tune_enabled = true;
+    c->tune_phase = bdpt_ctx::kTunePhases + 1;
+    return BDPT_OK;
+}
+
+int bdpt_stream_choice(const bdpt_ctx* c) { return c ? choice_of(c) : BDPT_EINVAL; }
+
 static int one_set_specialize(bdpt_ctx* c, int on) {
     if (!c) return BDPT_EINVAL;
     c->specialize = on != 0;
@@ -1088,6 +1114,15 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
     int tune_role = -1;
     bool pair = true;                                        // fused kernel: paired segment loads
     if (c->streams_req == 0 && c->tune_enabled) {
+        const bdpt_ctx* lead = c->tune_leader;
+        if (c->tune_phase == bdpt_ctx::kTunePhases && lead && lead->streams_req == 0 &&
+            lead->tune_phase == bdpt_ctx::kTunePhases + 1) {  // a group peer: devices[0] decided
+            c->tune_fused = lead->tune_fused;
+            c->tune_pair = lead->tune_pair;
+            c->tune_quarter = lead->tune_quarter;
+            c->tune_pool = lead->tune_pool;
+            c->tune_phase = bdpt_ctx::kTunePhases + 1;
+        }
         if (c->tune_phase == bdpt_ctx::kTunePhases) {        // waits for the last measured call
             if (int rc = fold_timing(c, c->tune_call[bdpt_ctx::kTunePhases - 1] + 1)) return rc;
             const double inf = std::numeric_limits<double>::infinity();
@@ -1287,7 +1322,9 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
             grid.z = 1;
             HIPCHK(c, hipEventRecord(c->rb_path_ev[half], c->stream));
             HIPCHK(c, hipStreamWaitEvent(c->fstream, c->rb_path_ev[half], 0));
-            HIPCHK(c, hipLaunchKernel((const void*)&bdpt_accum_kernel, grid, block, kargs, 0, c->fstream));
+            static const bool abl_nofold = getenv("BDPT_ABL_NOFOLD") != nullptr;   // ablation
+            if (!abl_nofold)
+                HIPCHK(c, hipLaunchKernel((const void*)&bdpt_accum_kernel, grid, block, kargs, 0, c->fstream));
             HIPCHK(c, hipEventRecord(c->rb_fold_ev[half], c->fstream));
             c->rb_used[half] = true;
             c->fold_last = half;
@@ -1631,6 +1668,7 @@ int bdpt_create_multi(bdpt_ctx** out, const bdpt_sphere* spheres, unsigned n, in
             snprintf(g_create_err, sizeof g_create_err, "%s", msg);
             return rc;
         }
+        p->tune_leader = c;
         c->peers.push_back(p);
     }
     if (int rc = group_set_shard(c, 0, 1, 8)) {
@@ -1701,6 +1739,21 @@ int bdpt_set_shard(bdpt_ctx* c, int shard, int nshards, int band_rows) {
 int bdpt_set_streams(bdpt_ctx* c, int streams) {
     if (int rc = one_set_streams(c, streams)) return rc;
     return forward(c, [&](bdpt_ctx* p) { return one_set_streams(p, streams); });
+}
+int bdpt_set_stream_choice(bdpt_ctx* c, int choice) {
+    if (int rc = one_set_stream_choice(c, choice)) return rc;
+    return forward(c, [&](bdpt_ctx* p) { return one_set_stream_choice(p, choice); });
+}
+// One device of the group: the kernel its last path-pass call ran and its stream-mode choice.
+int bdpt_device_mode(bdpt_ctx* c, int k, int* last_streams, int* features, int* choice) {
+    if (!c) return BDPT_EINVAL;
+    if (k < 0 || k > (int)c->peers.size())
+        return fail(c, BDPT_EINVAL, "bdpt_device_mode: device index %d of %d", k, 1 + (int)c->peers.size());
+    const bdpt_ctx* d = k == 0 ? c : c->peers[k - 1];
+    if (last_streams) *last_streams = d->last_streams;
+    if (features) *features = d->last_features;
+    if (choice) *choice = choice_of(d);
+    return BDPT_OK;
 }
 int bdpt_set_specialize(bdpt_ctx* c, int on) {
     if (int rc = one_set_specialize(c, on)) return rc;

@@ -1562,6 +1562,10 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                     unsigned xyv = xy;
                     asm volatile("" : "+v"(xyv));
                     const int li = kPool ? (int)lix : ((int)(xyv >> 16) - yoff) * a.W + (int)(xyv & 0xffffu);
+#ifdef BDPT_ABL_NOFOLD
+                    // ablation (results change): no radiance store -- the fold's upper bound
+                    if (__float_as_uint(rad.x) == 0x7fc00123u)
+#endif
                     a.rbuf[(size_t)(s0 + k * S) * a.nloc + (size_t)li] = r;
                 }
                 fresh = true;

@@ -114,6 +114,23 @@ int  bdpt_set_shard(bdpt_ctx *ctx, int shard, int nshards, int band_rows);
 int  bdpt_set_streams(bdpt_ctx *ctx, int streams);
 /* S used by the last bdpt_path_passes call. */
 int  bdpt_last_streams(const bdpt_ctx *ctx);
+/* The kernel variant the auto stream mode settled on, as BDPT_CHOICE_* bits (0 while it is still
+ * measuring, or when the stream mode is not auto).  bdpt_set_stream_choice applies such a choice
+ * without measuring (every device of a group); a later scene / shard / traversal / stream-mode
+ * change measures again.  No reference counterpart (smallpt_cpu.c:422 renders on one device): a
+ * multi-GPU job lets one device measure and gives every device its choice, so all GPUs run the
+ * same kernels -- the devices of a bdpt_create_multi group do this by themselves (they follow
+ * devices[0]); torchrun ranks pass rank 0's choice along (bench.py). */
+#define BDPT_CHOICE_DECIDED 1               /* a choice exists                                */
+#define BDPT_CHOICE_FUSED   2               /* the fused S = 1 kernel                         */
+#define BDPT_CHOICE_PAIRED  4               /* the fused variant with paired segment loads    */
+#define BDPT_CHOICE_QUARTER 8               /* pass streams with four passes per lane         */
+#define BDPT_CHOICE_POOLS  16               /* pass streams with pixel pools                  */
+int  bdpt_stream_choice(const bdpt_ctx *ctx);
+int  bdpt_set_stream_choice(bdpt_ctx *ctx, int choice);
+/* Device k of a (multi-device) context (0 = devices[0]): S and BDPT_FEAT_* bits of its last
+ * bdpt_path_passes call, and its BDPT_CHOICE_* bits. */
+int  bdpt_device_mode(bdpt_ctx *ctx, int k, int *last_streams, int *features, int *choice);
 /* Scene-specialised kernels (no reference counterpart; results are bit-identical): for scenes of
  * <= 64 spheres (brute-force traversal) the path kernel is compiled at run time (hipRTC, ~1 s, cached on disk) with the
  * sphere geometry folded in as constants.  1 = on (default), 0 = precompiled kernels only.  If

@@ -11,6 +11,13 @@ beside it.  The RCCL reduce is not included (it runs once per frame, not per ste
 
     python scripts/shard_probe.py [--scene cornell] [--passes 16] [--reps 3]
     python scripts/shard_probe.py --scene caustic --passes 128 --strong --streams 1,32
+    python scripts/shard_probe.py --workload weak64 [--passes 128] [--reps 3]
+
+--workload weak64 rehearses BASELINE configs[4] (bench.py `weak64`): synthetic64 at 4097x4097 cut
+into 8 FIXED bands of 512 rows, GPU r of 8 renders band r at the bench's passes per step.  Every band
+is timed as rank r of 8 on this one GPU; the one-GPU bench times band 0, and an 8-GPU step lasts as
+long as the slowest band, so the predicted weak-scaling efficiency is T1 / T8 = t(band 0) / max_r
+t(band r) (before the frame reduce).
 """
 import argparse
 import json
@@ -22,6 +29,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
 import gpu_bidirectional_raytracer_amd as g  # noqa: E402
+from gpu_bidirectional_raytracer_amd import sharding as shd  # noqa: E402
 
 
 WARM = 9
@@ -50,8 +58,38 @@ def run(sp, cam, W, H, sid, vlp, shard, nshards, band, streams, reps):
     return wall / reps, ms / reps, kms / reps, S
 
 
+def weak64(args):
+    """Per-band cost of configs[4]'s eight fixed 512-row bands (see the module docstring)."""
+    W, H, band, nb = 4097, 4097, 512, 8
+    cam, sp = g.read_scene(os.path.join(REPO, "assets", "scenes", "synthetic64.scn"))
+    g.update_camera(cam, W, H)
+    sched = g.PassScheduler()
+    sched.light()
+    sid, vlp = sched.next(args.passes * (args.reps + WARM))
+    rows = []
+    for r in range(nb):
+        wall, ms, kms, S = run(sp, cam, W, H, sid, vlp, r, nb, band, 0, args.reps)
+        rr = shd.owned_row_ranges(H, r, nb, band)               # band 0 also owns row 4096
+        px = shd.owned_pixels(W, H, r, nb, band)
+        rec = {"band": r, "rows": [list(x) for x in rr], "streams": S, "ms_per_step": round(wall, 3),
+               "path_ms": round(ms, 3), "kernel_ms": round(kms, 3),
+               "Msamples_s": round(px * args.passes / wall / 1e3, 1)}
+        rows.append(rec)
+        print(json.dumps(rec), flush=True)
+    t1, t8 = rows[0]["ms_per_step"], max(x["ms_per_step"] for x in rows)
+    slow = max(rows, key=lambda x: x["ms_per_step"])["band"]
+    print(json.dumps({"workload": "weak64", "passes_per_step": args.passes, "t1_band0_ms": t1,
+                      "t8_slowest_band_ms": t8, "slowest_band": slow,
+                      "predicted_weak_efficiency_T1_over_T8": round(t1 / t8, 4),
+                      "mean_band_ms": round(sum(x["ms_per_step"] for x in rows) / nb, 3),
+                      "note": "one GPU times each band as rank r of 8; the RCCL frame reduce is not included"}),
+          flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default=None, choices=["weak64"],
+                    help="weak64: time configs[4]'s eight fixed bands one after another")
     ap.add_argument("--scene", default="cornell")
     ap.add_argument("--passes", type=int, default=16)
     ap.add_argument("--reps", type=int, default=3)
@@ -60,6 +98,10 @@ def main():
     ap.add_argument("--streams", default="", help="S values to try besides auto, e.g. 1,2,8")
     ap.add_argument("--strong", action="store_true", help="same passes for every N (strong scaling)")
     args = ap.parse_args()
+    if args.workload == "weak64":
+        if args.passes == 16:                           # the bench's passes per step for weak64
+            args.passes = 128
+        return weak64(args)
     W, H = 1921, 1081
     cam, sp = g.read_scene(os.path.join(REPO, "assets", "scenes", args.scene + ".scn"))
     g.update_camera(cam, W, H)

@@ -111,3 +111,46 @@ def test_device_timing_through_the_abi():
         assert d["path_ms"] >= d["kernel_ms"] > 0
         assert d["owned_pixels"] == shd.owned_pixels(W, H, 1, 3, 8) == 16 * W    # bands 1 and 4
         assert g._lib.lib.bdpt_device_timing(r._h, 1, None, None, None, None, None) != 0   # one device only
+
+
+def test_reduce_fallback_rule():
+    """an in-process run on distinct GPUs whose frame reduce is not RCCL is a
+    fallback (bench.py exits unless --allow-peer-reduce); repeated devices are a rehearsal."""
+    assert bench.is_reduce_fallback("inproc", [0, 1], "peer", False)
+    assert not bench.is_reduce_fallback("inproc", [0, 1], "rccl", False)
+    assert not bench.is_reduce_fallback("inproc", [0, 0], "peer", False)
+    assert not bench.is_reduce_fallback("single", [0], "none", False)
+    assert bench.is_reduce_fallback("ranks", [0], "none", True)
+    assert not bench.is_reduce_fallback("ranks", [0], "none", False)
+
+
+def test_stream_choice_through_the_abi():
+    """bdpt_stream_choice / bdpt_set_stream_choice / bdpt_device_mode on a host-CPU context: a
+    choice applied without measuring reads back, a bad one or a non-auto stream mode is refused,
+    and the per-device mode names S, the kernel features and the choice."""
+    import gpu_bidirectional_raytracer_amd as g
+    from gpu_bidirectional_raytracer_amd import _lib as L
+    from conftest import SCENES
+    cam, sp = g.read_scene(os.path.join(SCENES, "simple.scn"))
+    g.update_camera(cam, 16, 8)
+    with g.Renderer(sp, 16, 8, cam, device=-1) as r:
+        assert r.stream_choice == 0                               # nothing measured yet
+        ch = 1 | 16                                               # decided, pixel pools
+        r.set_stream_choice(ch)
+        assert r.stream_choice == ch
+        assert r.device_mode(0)["choice"] == ["decided", "pools"]
+        for bad in (0, 16, 64):                                   # not decided / unknown bits
+            with pytest.raises(g.BdptError):
+                r.set_stream_choice(bad)
+        r.set_streams(1)                                          # fused fixed: no auto choice
+        assert r.stream_choice == 0
+        with pytest.raises(g.BdptError):
+            r.set_stream_choice(ch)
+        r.light_pass(0)
+        sid, vlp = g.PassScheduler().next(2)
+        r.path_passes(sid, vlp)
+        m = r.device_mode(0)
+        assert m["streams"] == 1 and m["choice"] == []
+        with pytest.raises(g.BdptError):
+            r.device_mode(1)
+    assert L.CHOICES[16] == "pools"

@@ -116,3 +116,27 @@ def test_smallpt_host_on_several_devices(gpu, tmp_path, devs):
     assert r.returncode == 0, r.stderr
     assert ("rccl" if devs == "0" else "peer") in r.stderr
     assert filecmp.cmp(a, b, shallow=False)
+
+
+def test_group_devices_follow_devices0_stream_choice(gpu):
+    """the peers of a group take devices[0]'s auto stream-mode decision, so every
+    device runs the same kernel; the frame still equals the one-device frame bit for bit."""
+    W, H = 321, 241
+    cam, sp = g.read_scene(os.path.join(SCENES, "caustic.scn"))
+    g.update_camera(cam, W, H)
+    sid, vlp = schedule(16 * 10)
+    with g.Renderer(sp, W, H, cam, devices=[gpu, gpu, gpu]) as r:
+        r.set_streams(0)
+        r.light_pass(0)
+        for k in range(10):                                       # 8 measured calls, then the choice
+            r.path_passes(sid[16 * k:16 * (k + 1)], vlp[16 * k:16 * (k + 1)])
+        modes = [r.device_mode(k) for k in range(3)]
+        assert "decided" in modes[0]["choice"]
+        assert all(m == modes[0] for m in modes), modes
+        col, cnt = r.read_radiance()
+        # a rank applies rank 0's choice: the same bits, no measurement
+        r.set_stream_choice(r.stream_choice)
+        assert r.device_mode(2)["choice"] == modes[0]["choice"]
+    ref = render("caustic", W, H, sid, vlp, device=gpu)
+    same(col, ref[0], "colors")
+    same(cnt, ref[1], "counter")
