@@ -45,6 +45,20 @@ extern "C" __global__ void bdpt_light_kernel(const bdpt_dev_sphere*, unsigned, c
 extern "C" const void* bdpt_path_kernel_table[36];   // [(S > 1) * 18 + (BVH ? 17 : n <= 16 ? n : 0)]
 extern "C" __global__ void bdpt_pixels_kernel(const bdpt_dev_vec*, uchar4*, const float*, int);
 extern "C" __global__ void bdpt_accum_kernel(bdpt_path_args);
+extern "C" __global__ void bdpt_accum_nt_kernel(bdpt_path_args);
+extern "C" __global__ void bdpt_accum_nt8_kernel(bdpt_path_args);
+extern "C" __global__ void bdpt_accum_u8_kernel(bdpt_path_args);
+// the fold kernel (BDPT_FOLD_KIND = nt | nt8 | u8: experiments)
+static const void* fold_kernel() {
+    static const void* k = [] {
+        const char* e = getenv("BDPT_FOLD_KIND");
+        if (e && !strcmp(e, "nt")) return (const void*)&bdpt_accum_nt_kernel;
+        if (e && !strcmp(e, "nt8")) return (const void*)&bdpt_accum_nt8_kernel;
+        if (e && !strcmp(e, "u8")) return (const void*)&bdpt_accum_u8_kernel;
+        return (const void*)&bdpt_accum_kernel;
+    }();
+    return k;
+}
 extern "C" __global__ void bdpt_frame_add_kernel(float*, const float*, unsigned*, const unsigned*, int);
 
 // gamma thresholds (host, once): see bdpt_util.c
@@ -129,6 +143,11 @@ struct bdpt_ctx {
     unsigned* d_poolctr = nullptr;      // pixel pools: claimed pixels per pass and eighth, a line each,
                                         // two sets: a pooled launch uses one and zeroes the other
     int pool_set = 0;                   // the set the next pooled launch uses
+    unsigned* d_uflags = nullptr;       // ordered in-kernel fold (units): per 8x8 wave tile, epoch << 8 | range
+    size_t uflags_cap = 0;
+    unsigned uepoch = 0;                // launches of the units kernel (flag tags)
+    unsigned* d_uerr = nullptr;         // set by a unit whose handover wait timed out
+    bool units_check = false;           // a units launch ran since the last error check
     int traversal = BDPT_TRAVERSE_AUTO; // bdpt_set_traversal
     bool has_bvh = false;               // the scene has a BVH (bdpt_bvh.cpp)
     int bvh_nn = 0, bvh_ns = 0, big_n = 0;
@@ -167,7 +186,7 @@ struct bdpt_ctx {
         hipFunction_t fn = nullptr;
         int waves = 0;
         std::string flags, err;
-    } jit_memo[3][2];
+    } jit_memo[4][2];
     int last_features = 0;              // BDPT_FEAT_* of the last path-pass launch
     unsigned rand_seed = 0;             // seed of the current MT607 table (rand_ready)
     char err[512] = {0};
@@ -302,7 +321,7 @@ static int upload_scene(bdpt_ctx* c) {
 
 static void release(bdpt_ctx* c) {
     void* bufs[] = {c->d_params, c->d_rand, c->d_rndp, c->d_lp, c->d_sph, c->d_lights, c->d_geom, c->d_lightrec, c->d_colors,
-                    c->d_counter, c->d_pixels, c->d_thr, c->d_rbuf, c->d_poolctr, c->d_bvh_nodes,
+                    c->d_counter, c->d_pixels, c->d_thr, c->d_rbuf, c->d_poolctr, c->d_uflags, c->d_uerr, c->d_bvh_nodes,
                     c->d_bvh_geom, c->d_big_geom, c->d_mat, c->d_bvh_ids, c->d_big_ids,
                     c->d_fcolors, c->d_fcounter, c->d_fpixels, c->d_ftmp, c->d_ftmpc};
     for (void* b : bufs)
@@ -556,7 +575,16 @@ static void pool_shape(long nloc, int* R, int* G) {
 
 // The specialised kernel for the context's scene and pass-stream mode, compiled on first use;
 // nullptr = use the precompiled instance (reason in c->jit_err).
-static hipFunction_t jit_path_kernel_build(bdpt_ctx* c, bool streams, bool pair, bool pool) {
+// Pass streams with the ordered fold inside the kernel (bdpt_kernels.hip BDPT_UNITS): BDPT_UNITS=P
+// forces it with ranges of P passes (experiments; 0 = never).
+static int units_env() {
+    const char* e = getenv("BDPT_UNITS");
+    if (!e || !*e) return -1;
+    const int v = atoi(e);
+    return v < 1 ? 0 : (v > 128 ? 128 : v);
+}
+
+static hipFunction_t jit_path_kernel_build(bdpt_ctx* c, bool streams, bool pair, bool pool, bool units) {
     const unsigned n = (unsigned)c->spheres.size();
     if (!c->specialize || n < 1 || n > 64) return nullptr;          // kJitEmis is 64 bits
     unsigned long long emis = 0;
@@ -613,6 +641,7 @@ static hipFunction_t jit_path_kernel_build(bdpt_ctx* c, bool streams, bool pair,
         if (!streams) all.push_back("-DBDPT_FUSED_WAVES=" + std::to_string(waves));
         if (!streams && !pair) all.push_back("-DBDPT_RNG_PAIR=0");
         if (streams && pool) all.push_back("-DBDPT_POOL=1");
+        if (streams && units) all.push_back("-DBDPT_UNITS=1");
         if (const char* extra = getenv("BDPT_JIT_FLAGS")) {    // experiments: extra -D options
             std::string tok;
             for (const char* q = extra;; q++) {
@@ -635,7 +664,7 @@ static hipFunction_t jit_path_kernel_build(bdpt_ctx* c, bool streams, bool pair,
         int stat = 0;
         if (!coarse && !user_coarse &&
             hipFuncGetAttribute(&stat, HIP_FUNC_ATTRIBUTE_SHARED_SIZE_BYTES, fn) == hipSuccess) {
-            const size_t slots = streams ? 1 : (size_t)fused_max_passes();
+            const size_t slots = units ? (size_t)std::max(units_env(), 16) : streams ? 1 : (size_t)fused_max_passes();
             const size_t dyn = sizeof(float4) * (4 * (size_t)n + 3 * slots + 5 + 4 * 128 * 2) + sizeof(unsigned) * slots;
             const size_t lds = 160 * 1024, fine = lds / (dyn + stat), half = lds / (dyn + stat - 2048);
             if (fine < (size_t)waves && half > fine) {
@@ -677,15 +706,16 @@ static std::string jit_env_key() {
     return k;
 }
 
-static hipFunction_t jit_path_kernel(bdpt_ctx* c, bool streams, bool pair = true, bool pool = false) {
+static hipFunction_t jit_path_kernel(bdpt_ctx* c, bool streams, bool pair = true, bool pool = false,
+                                     bool units = false) {
     const std::string key = jit_env_key();
-    bdpt_ctx::jit_memo_t& m = c->jit_memo[streams ? (pool ? 2 : 1) : 0][pair];
+    bdpt_ctx::jit_memo_t& m = c->jit_memo[streams ? (units ? 3 : pool ? 2 : 1) : 0][pair];
     if (m.valid && m.flags == key) {
         snprintf(c->jit_err, sizeof c->jit_err, "%s", m.err.c_str());
         if (m.fn) { c->jit_waves = m.waves; c->jit_zero_exit = m.zero_exit; }
         return m.fn;
     }
-    hipFunction_t fn = jit_path_kernel_build(c, streams, pair, streams && pool);
+    hipFunction_t fn = jit_path_kernel_build(c, streams, pair, streams && pool, streams && units);
     m.valid = true;
     m.fn = fn;
     m.waves = c->jit_waves;
@@ -1188,6 +1218,10 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
                                          (tune_role >= 6 || (tune_role < 0 && c->tune_phase == bdpt_ctx::kTunePhases + 1 &&
                                                              c->tune_pool))));
     if (want_pool) S = chunk < npass ? chunk : npass;        // one pass per lane slice
+    // ordered in-kernel fold (units of a tile and a range of passes; no radiance buffer): forced by
+    // BDPT_UNITS=P (ranges of P passes)
+    const int uenv = units_env();
+    const bool want_units = !bvh && S > 1 && !want_pool && uenv > 0;
     c->last_streams = S;
     const int kidx = bvh ? 17 : (a.n <= 16 ? (int)a.n : 0);
     if (bvh) {
@@ -1199,7 +1233,7 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
         a.bvh_q = c->bvh_q;
     }
     c->last_bvh = bvh;
-    if (S > 1) {
+    if (S > 1 && !want_units) {
         const int cmax = npass < chunk ? npass : chunk;
         const size_t need = (size_t)cmax * (size_t)lanes;
         if (need > c->rbuf_cap) {
@@ -1224,7 +1258,7 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
         cs.kev.push_back(e);
     }
     // resolve the specialised kernels (a compile on first use) before the timed region starts
-    hipFunction_t jf_streams = nullptr, jf_fused = nullptr, jf_pool = nullptr;
+    hipFunction_t jf_streams = nullptr, jf_fused = nullptr, jf_pool = nullptr, jf_units = nullptr;
     bool any_fused = false, pool_ran = false;
     for (int p0 = 0; grid_rows > 0 && p0 < npass; p0 += chunk) {
         const int np = npass - p0 < chunk ? npass - p0 : chunk;
@@ -1232,12 +1266,13 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
         any_fused |= !st;
         if (bvh) continue;
         if (st && want_pool && !jf_pool) jf_pool = jit_path_kernel(c, true, true, true);
-        if (st && !jf_pool && !jf_streams) jf_streams = jit_path_kernel(c, true);
+        if (st && want_units && !jf_units) jf_units = jit_path_kernel(c, true, true, false, true);
+        if (st && !jf_pool && !jf_units && !jf_streams) jf_streams = jit_path_kernel(c, true);
         if (!st && !jf_fused) jf_fused = jit_path_kernel(c, false, pair);
     }
     // a fused launch updates colors itself: it waits for the outstanding fold, before the call's
     // timing starts (so the stream-mode measurement does not charge that fold to it)
-    if (any_fused)
+    if (any_fused || jf_units)
         if (int rc = join_fold(c)) return rc;
     HIPCHK(c, hipEventRecord(cs.ev0, c->stream));
     int launches = 0;
@@ -1261,9 +1296,11 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
         // S per launch: a short last chunk gets no idle stream slices
         const bool st = (S < a.npass ? S : a.npass) > 1;     // the pass-stream kernel
         const bool pooled = st && jf_pool != nullptr;        // its pixel-pool build
+        const bool unitsl = st && jf_units != nullptr;       // its ordered in-kernel fold build
         a.streams = S < a.npass ? S : a.npass;
+        if (unitsl) a.unit_passes = uenv < a.npass ? uenv : a.npass;
         // a workgroup stages the VLPs and sids of its own passes only (bdpt_kernels.hip nslot)
-        const size_t slots = ((size_t)a.npass + a.streams - 1) / a.streams;
+        const size_t slots = unitsl ? (size_t)a.unit_passes : ((size_t)a.npass + a.streams - 1) / a.streams;
         size_t smem = sizeof(float4) * (tab + 3 * slots + 5 + 4 * 128 * 2)
                       + sizeof(unsigned) * (slots + ids);
         if (const char* pad = getenv("BDPT_SMEM_PAD"))       // experiments: cap workgroups per CU
@@ -1271,15 +1308,19 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
         if (smem > 160 * 1024)
             return fail(c, BDPT_EINVAL, "bdpt_path_passes: scene too large for LDS (%u spheres)", a.n);
         const void* kern = bdpt_path_kernel_table[st * 18 + kidx];
-        const hipFunction_t jf = st ? (pooled ? jf_pool : jf_streams) : jf_fused;
+        const hipFunction_t jf = st ? (pooled ? jf_pool : unitsl ? jf_units : jf_streams) : jf_fused;
         c->last_specialized = jf != nullptr;
         c->last_features = BDPT_FEAT_LAST_SKIP | (bvh ? BDPT_FEAT_BVH : 0) | (st ? BDPT_FEAT_STREAMS : 0) |
-                           (pooled ? BDPT_FEAT_POOLS : 0) |
+                           (pooled ? BDPT_FEAT_POOLS : 0) | (unitsl ? BDPT_FEAT_UNITS : 0) |
                            (jf ? BDPT_FEAT_SPECIALIZED | BDPT_FEAT_DET_SKIP | (c->jit_zero_exit ? BDPT_FEAT_ZERO_EXIT : 0) : 0);
         void* kargs[] = {&a};
         grid.z = a.streams;
         const int half = c->rb_next;
-        if (st) {
+        if (unitsl) {
+            // the units fold in the kernel: no radiance buffer; the previous call's folds were
+            // joined above
+            a.rbuf = nullptr;
+        } else if (st) {
             // this half was last read by the fold of the launch before the previous one
             if (c->rb_used[half]) HIPCHK(c, hipStreamWaitEvent(c->stream, c->rb_fold_ev[half], 0));
             a.rbuf = c->d_rbuf + (size_t)half * c->rbuf_cap;
@@ -1311,6 +1352,36 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
             pgrid = dim3((unsigned)(per * a.streams), 1, 1);
             pool_ran = true;
         }
+        if (unitsl) {
+            // 1-D grid of units in range-major order: workgroup b renders tile b % wgs, range b / wgs
+            const int wgs = (int)grid.x * grid_rows;
+            const int nranges = (a.npass + a.unit_passes - 1) / a.unit_passes;
+            const size_t nflags = (size_t)wgs * 4;
+            if (!c->d_uerr) {
+                HIPCHK(c, hipMalloc(&c->d_uerr, sizeof(unsigned)));
+                HIPCHK(c, hipMemsetAsync(c->d_uerr, 0, sizeof(unsigned), c->stream));
+            }
+            if (nflags > c->uflags_cap || ((c->uepoch + 1) & 0xffffffu) == 0) {
+                if (nflags > c->uflags_cap) {
+                    HIPCHK(c, hipStreamSynchronize(c->stream));
+                    if (c->d_uflags) HIPCHK(c, hipFree(c->d_uflags));
+                    c->d_uflags = nullptr;
+                    HIPCHK(c, hipMalloc(&c->d_uflags, sizeof(unsigned) * nflags));
+                    c->uflags_cap = nflags;
+                }
+                HIPCHK(c, hipMemsetAsync(c->d_uflags, 0, sizeof(unsigned) * c->uflags_cap, c->stream));
+                c->uepoch = 0;
+            }
+            c->uepoch++;                                     // tags never repeat within 2^24 launches
+            a.unit_tag = c->uepoch << 8;
+            a.unit_flags = c->d_uflags;
+            a.unit_err = c->d_uerr;
+            a.unit_wgs = wgs;
+            a.gx = (int)grid.x;
+            a.gy = grid_rows;
+            pgrid = dim3((unsigned)(wgs * nranges), 1, 1);
+            c->units_check = true;
+        }
         HIPCHK(c, hipEventRecord(cs.kev[2 * launches], c->stream));
         if (jf)
             HIPCHK(c, hipModuleLaunchKernel(jf, pgrid.x, pgrid.y, pgrid.z, block.x, 1, 1, (unsigned)smem,
@@ -1318,13 +1389,13 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
         else
             HIPCHK(c, hipLaunchKernel(kern, grid, block, kargs, smem, c->stream));
         HIPCHK(c, hipEventRecord(cs.kev[2 * launches + 1], c->stream));
-        if (st) {                                           // the ordered fold, on fstream
+        if (st && !unitsl) {                                // the ordered fold, on fstream
             grid.z = 1;
             HIPCHK(c, hipEventRecord(c->rb_path_ev[half], c->stream));
             HIPCHK(c, hipStreamWaitEvent(c->fstream, c->rb_path_ev[half], 0));
             static const bool abl_nofold = getenv("BDPT_ABL_NOFOLD") != nullptr;   // ablation
             if (!abl_nofold)
-                HIPCHK(c, hipLaunchKernel((const void*)&bdpt_accum_kernel, grid, block, kargs, 0, c->fstream));
+                HIPCHK(c, hipLaunchKernel(fold_kernel(), grid, block, kargs, 0, c->fstream));
             HIPCHK(c, hipEventRecord(c->rb_fold_ev[half], c->fstream));
             c->rb_used[half] = true;
             c->fold_last = half;
@@ -1356,6 +1427,13 @@ static int one_synchronize(bdpt_ctx* c) {
     HIPCHK(c, hipSetDevice(c->device));
     if (int rc = join_fold(c)) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->units_check) {                                  // a unit's handover wait timed out?
+        unsigned e = 0;
+        HIPCHK(c, hipMemcpy(&e, c->d_uerr, sizeof e, hipMemcpyDeviceToHost));
+        c->units_check = false;
+        if (e) return fail(c, BDPT_EHIP, "path kernel: a unit waited too long for its tile's previous range "
+                                         "(in-order workgroup dispatch assumed; the frame is not valid)");
+    }
     return fold_timing(c);
 }
 

@@ -336,6 +336,10 @@ __device__ __forceinline__ f3 cosine_tail(f3 w, f3 u, float u_phi, float u_r2, f
 #ifndef BDPT_RNG_PAIR
 #define BDPT_RNG_PAIR 1
 #endif
+// pass streams: radiance stores to the fold buffer with the nontemporal (streaming) hint
+#ifndef BDPT_RBUF_NT
+#define BDPT_RBUF_NT 0
+#endif
 // pass streams: parked lanes load their next pass's randoms at park time (see the loop)
 #ifndef BDPT_PARK_LOAD
 #define BDPT_PARK_LOAD 1
@@ -356,6 +360,11 @@ __device__ __forceinline__ f3 cosine_tail(f3 w, f3 u, float u_phi, float u_r2, f
 // launch's passes, lanes carrying their pass, measured slower at one GPU: caustic >= 16 %.)
 #ifndef BDPT_POOL
 #define BDPT_POOL 0
+#endif
+// Pass streams with the ordered fold inside the kernel (a build with BDPT_UNITS; bdpt_host.cpp
+// launches it as a 1-D grid of units, bdpt_path_args.unit_*): no radiance buffer, no fold kernel.
+#ifndef BDPT_UNITS
+#define BDPT_UNITS 0
 #endif
 #ifndef BDPT_POOL_FDIV
 #define BDPT_POOL_FDIV 1
@@ -589,6 +598,32 @@ __device__ __forceinline__ void unroll_down(F& f) {
     }
 }
 
+// Handover between the units of a tile (BDPT_UNITS): agent-scope relaxed atomics are coherent
+// across XCDs (sc1 loads / stores on gfx950, no L2 invalidation); the producer waits for its data
+// stores (s_waitcnt vmcnt(0)) before it stores the flag.
+__device__ __forceinline__ float ld_coherent(float* p) {
+    return __uint_as_float(__hip_atomic_load((unsigned*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void st_coherent(float* p, float v) {
+    __hip_atomic_store((unsigned*)p, __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Wait until *f == want.  The unit that sets it has a smaller workgroup id, so it was dispatched
+// earlier and is resident or done; the bound (~0.3 s) turns a broken assumption into an error
+// report (*err) instead of a hang.
+__device__ __forceinline__ void unit_wait(unsigned* f, unsigned want, unsigned* err) {
+    for (unsigned spins = 0;; spins++) {
+        const unsigned v = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        if (v == want) break;
+        if (spins > (1u << 20)) {
+            __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(10);
+    }
+    asm volatile("" ::: "memory");
+}
+
 __device__ __forceinline__ void wave_lds_fence() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -700,10 +735,21 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
     // pixel pools: a 1-D grid with the passes interleaved, so every pass has workgroups from the
     // launch's start to its end and the passes finish together (z-major, the last passes ran at
     // the end on their own workgroups); pass (b / 8) mod S keeps each pass on all 8 XCDs
-    const int S = STREAMS ? a.streams : 1;
-    const int s0 = !STREAMS ? 0 : kPool ? (int)((blockIdx.x >> 3) % (unsigned)S) : (int)blockIdx.z;
-    const int nslot = (a.npass - s0 + S - 1) / S;
-    const int mslot = (a.npass + S - 1) / S;         // slots of the LDS layout (any s0)
+    // ordered in-kernel fold (BDPT_UNITS builds): a 1-D grid of units (tile, range) in range-major
+    // order; a lane renders the range's passes of its pixel in order and keeps the running mean in
+    // registers, and the units of a tile follow each other through per-wave-tile flags
+    constexpr bool kUnits = STREAMS && BDPT_UNITS && !BDPT_POOL;
+    const unsigned urange = kUnits ? blockIdx.x / (unsigned)a.unit_wgs : 0u;
+    const int vtile = kUnits ? (int)(blockIdx.x - urange * (unsigned)a.unit_wgs) : 0;
+    // the workgroup's tile (vbx, vby) in the tile grid (vgx, vgy)
+    const int vbx = kUnits ? vtile % a.gx : (int)blockIdx.x, vby = kUnits ? vtile / a.gx : (int)blockIdx.y;
+    const int vgx = kUnits ? a.gx : (int)gridDim.x, vgy = kUnits ? a.gy : (int)gridDim.y;
+    const int S = kUnits ? 1 : (STREAMS ? a.streams : 1);
+    const int s0 = kUnits ? (int)urange * a.unit_passes
+                 : !STREAMS ? 0 : kPool ? (int)((blockIdx.x >> 3) % (unsigned)S) : (int)blockIdx.z;
+    const int nslot = kUnits ? (a.npass - s0 < a.unit_passes ? a.npass - s0 : a.unit_passes)
+                             : (a.npass - s0 + S - 1) / S;
+    const int mslot = kUnits ? a.unit_passes : (a.npass + S - 1) / S;   // slots of the LDS layout (any s0)
     float4* C = smem;                 // {cx, cy, cz, bits(refl | emissive<<8)}
     float4* E = smem + n;             // {ex, ey, ez, rad}
     float4* P = smem + 2 * n;         // {px, py, pz, 0}  (hit normal)
@@ -817,8 +863,8 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
 #else
 #define BDPT_TICK(k) do { } while (0)
 #endif
-    int x = blockIdx.x * BDPT_BTW + (wave % BDPT_BLOCK_WX) * BDPT_WTW + (lane % BDPT_WTW);
-    int ly = blockIdx.y * BDPT_BTH + (wave / BDPT_BLOCK_WX) * BDPT_WTH + (lane / BDPT_WTW);
+    int x = vbx * BDPT_BTW + (wave % BDPT_BLOCK_WX) * BDPT_WTW + (lane % BDPT_WTW);
+    int ly = vby * BDPT_BTH + (wave / BDPT_BLOCK_WX) * BDPT_WTH + (lane / BDPT_WTW);
 #if BDPT_PACK_EDGES
     // Frame edges packed into full waves (rows not remapped to shard bands): a frame whose width
     // leaves tw <= 8 columns in the last workgroup column (1921 = 60 x 32 + 1) would give every
@@ -827,21 +873,21 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
     // rows of the last workgroup row (x below the last column, row-major) to the workgroups of
     // that row.  Every pixel is still rendered by exactly one lane.
     if (a.tiles_per_band <= 0) {
-        const int gx = (int)gridDim.x, gy = (int)gridDim.y;
+        const int gx = vgx, gy = vgy;
         const int xt = (gx - 1) * BDPT_BTW, yt = (gy - 1) * BDPT_BTH;
         const int tw = a.W - xt, th = a.H - yt, wl = (int)threadIdx.x;
-        if (tw <= BDPT_WTW && (int)blockIdx.x == gx - 1) {
-            const int q = (int)blockIdx.y * 256 + wl;
+        if (tw <= BDPT_WTW && vbx == gx - 1) {
+            const int q = vby * 256 + wl;
             x = xt + q % tw;
             ly = q / tw;
-        } else if (th < BDPT_BTH && (int)blockIdx.x < gx - 1 && (int)blockIdx.y == gy - 1) {
-            const int q = (int)blockIdx.x * 256 + wl;
+        } else if (th < BDPT_BTH && vbx < gx - 1 && vby == gy - 1) {
+            const int q = vbx * 256 + wl;
             x = q % xt;
             ly = yt + q / xt;
         }
     }
 #endif
-    const int yoff = (bdpt_dev_tile_row(a, blockIdx.y) - (int)blockIdx.y) * BDPT_BTH;   // uniform
+    const int yoff = (bdpt_dev_tile_row(a, vby) - vby) * BDPT_BTH;   // uniform
     int y = ly + yoff;
     bool active = x < a.W && y < a.H;
     if (active && a.nshards > 1) active = ((y / a.band_rows) % a.nshards) == a.shard;
@@ -918,7 +964,20 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
 
     f3 col = mk(0.f, 0.f, 0.f);
     unsigned cnt0 = 0;                // the counter before pass p is cnt0 + p
-    if (active) {
+    // (units: the counter before the unit's slot k is cnt0 + k)
+    const unsigned uflag = kUnits ? (unsigned)vtile * 4u + (unsigned)wave : 0u;   // this wave's 8x8 tile
+    if constexpr (kUnits) {
+        // the previous range of this tile has folded its passes (in-order WG dispatch makes that a
+        // short or no wait); colours and counter are read at the coherence point (agent-scope
+        // relaxed atomics: the previous unit may have run on another XCD, whose L2 is not ours)
+        if (urange > 0) unit_wait(a.unit_flags + uflag, a.unit_tag | urange, a.unit_err);
+        if (active) {
+            col.x = ld_coherent(&a.colors[i].x);
+            col.y = ld_coherent(&a.colors[i].y);
+            col.z = ld_coherent(&a.colors[i].z);
+            cnt0 = __hip_atomic_load(&a.counter[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    } else if (active) {
         if constexpr (!STREAMS) {
             const bdpt_dev_vec cv = a.colors[i];
             col = mk(cv.x, cv.y, cv.z);
@@ -975,7 +1034,7 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
     if constexpr (kParkPf) load_cam(j);
     f3 ro = mk(0.f, 0.f, 0.f), rd = ro, thr = ro, rad = ro, nl = ro;
     bool specular = true, fresh = true, parked = false, want = kPool && !active;
-    bool alive = active && nslot > 0 && cnt0 + (unsigned)(s0 + k * S) < BDPT_DEV_COUNTER_CAP;
+    bool alive = active && nslot > 0 && cnt0 + (unsigned)(kUnits ? k : s0 + k * S) < BDPT_DEV_COUNTER_CAP;
 
     // (a pool lane without a pixel yet keeps the loop going: it draws one at the iteration's end)
     while (__builtin_amdgcn_ballot_w64(alive || (kPool && want)) != 0) {   // wave-uniform loop
@@ -1545,7 +1604,7 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
         if (alive) {
             if (!done && ++depth > 6) done = true;                       // :621 7-segment cap
             if (done) {                                                  // :774-787
-                if constexpr (!STREAMS) {
+                if constexpr (!STREAMS || kUnits) {
                     const unsigned cnt = cnt0 + (unsigned)k;      // S == 1: pass k
                     if (cnt == 0) {
                         col = rad;
@@ -1566,7 +1625,18 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                     // ablation (results change): no radiance store -- the fold's upper bound
                     if (__float_as_uint(rad.x) == 0x7fc00123u)
 #endif
-                    a.rbuf[(size_t)(s0 + k * S) * a.nloc + (size_t)li] = r;
+                    {
+                    bdpt_dev_vec* rp = a.rbuf + (size_t)(s0 + k * S) * a.nloc + (size_t)li;
+#if BDPT_RBUF_NT
+                    // streaming stores: the radiance is read once, by the fold, long after -- keep
+                    // it from displacing the random table's lines in L2
+                    __builtin_nontemporal_store(r.x, &rp->x);
+                    __builtin_nontemporal_store(r.y, &rp->y);
+                    __builtin_nontemporal_store(r.z, &rp->z);
+#else
+                    *rp = r;
+#endif
+                    }
                 }
                 fresh = true;
                 depth = 0;
@@ -1576,7 +1646,8 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                 } else {
                     k++;
                     const int pn = s0 + k * S;
-                    alive = pn < a.npass && cnt0 + (unsigned)pn < BDPT_DEV_COUNTER_CAP;
+                    alive = kUnits ? (k < nslot && cnt0 + (unsigned)k < BDPT_DEV_COUNTER_CAP)
+                                   : (pn < a.npass && cnt0 + (unsigned)pn < BDPT_DEV_COUNTER_CAP);
                     if constexpr (kRegen) {
                         parked = alive;
                         alive = false;
@@ -1683,6 +1754,21 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
         atomicAdd(&a.prof[7], 1ull);
     }
 #endif
+    if constexpr (kUnits) {
+        // the unit's result, then this wave tile's flag: the next range's unit may start
+        if (active && k > 0) {
+            st_coherent(&a.colors[i].x, col.x);
+            st_coherent(&a.colors[i].y, col.y);
+            st_coherent(&a.colors[i].z, col.z);
+            __hip_atomic_store(&a.counter[i], cnt0 + (unsigned)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            a.pixels[i] = bdpt_dev_to_rgba(col.x, col.y, col.z, a.gamma_thr);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");          // the stores above are performed
+        if (lane == 0)
+            __hip_atomic_store(a.unit_flags + uflag, a.unit_tag | (urange + 1u), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
     if (STREAMS || !active || k == 0) return;                            // nothing rendered
     const unsigned cnt = cnt0 + (unsigned)k;
     bdpt_dev_vec out;
@@ -1706,7 +1792,8 @@ extern "C" const void* bdpt_path_kernel_table[36] = {BDPT_ROW(false), BDPT_ROW(t
 // Ordered fold of pass-stream radiance (S > 1): the running mean of device.cu:774-787 applied
 // to rbuf[0..npass) in pass order, so the result is the S == 1 result bit for bit.  Same grid
 // rows (and shard remap) as the path launch; one thread per pixel.
-extern "C" __global__ __launch_bounds__(256) void bdpt_accum_kernel(bdpt_path_args a) {
+template <bool NT, int U>
+__device__ __forceinline__ void accum_body(const bdpt_path_args& a) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #ifdef BDPT_PROF
     // section profile (experiments): shader cycles per wave between wave-uniform points, summed
@@ -1745,12 +1832,38 @@ extern "C" __global__ __launch_bounds__(256) void bdpt_accum_kernel(bdpt_path_ar
     };
     // (a version with 8 loads in flight ran faster alone but slowed the overlapped path kernel
     // of the next launch: caustic8 -1.3 %)
-    for (int p = 0; p < n; p++) fold(rb[(size_t)p * a.nloc]);
+    auto ld = [&](int p) -> bdpt_dev_vec {
+        const bdpt_dev_vec* q = rb + (size_t)p * a.nloc;
+        if constexpr (NT) {
+            bdpt_dev_vec v;
+            v.x = __builtin_nontemporal_load(&q->x);
+            v.y = __builtin_nontemporal_load(&q->y);
+            v.z = __builtin_nontemporal_load(&q->z);
+            return v;
+        }
+        return *q;
+    };
+    int p = 0;
+    if constexpr (U > 1) {
+        for (; p + U <= n; p += U) {
+            bdpt_dev_vec v[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) v[u] = ld(p + u);
+#pragma unroll
+            for (int u = 0; u < U; u++) fold(v[u]);
+        }
+    }
+    for (; p < n; p++) fold(ld(p));
     if (cnt == cnt0) return;
     a.colors[i] = col;
     a.counter[i] = cnt;
     a.pixels[i] = bdpt_dev_to_rgba(col.x, col.y, col.z, a.gamma_thr);
 }
+extern "C" __global__ __launch_bounds__(256) void bdpt_accum_kernel(bdpt_path_args a) { accum_body<false, 1>(a); }
+// fold variants (experiments, BDPT_FOLD_KIND): streaming loads, loads in flight
+extern "C" __global__ __launch_bounds__(256) void bdpt_accum_nt_kernel(bdpt_path_args a) { accum_body<true, 1>(a); }
+extern "C" __global__ __launch_bounds__(256) void bdpt_accum_nt8_kernel(bdpt_path_args a) { accum_body<true, 8>(a); }
+extern "C" __global__ __launch_bounds__(256) void bdpt_accum_u8_kernel(bdpt_path_args a) { accum_body<false, 8>(a); }
 
 // Frame assembly of a multi-device context without RCCL: add a peer's zero-padded frame (exact:
 // each pixel is non-zero on one device only, and x + 0 == x).

@@ -162,6 +162,9 @@ int  bdpt_last_traversal(const bdpt_ctx *ctx);
 #define BDPT_FEAT_STREAMS    32             /* pass streams (one pass per lane + ordered fold)*/
 #define BDPT_FEAT_POOLS      64             /* pass streams with pixel pools (lanes restart on
                                                new pixels of their pass, claimed in chunks)   */
+#define BDPT_FEAT_UNITS     128             /* pass streams with the ordered fold in the kernel:
+                                               units of (tile, range of passes) in range order,
+                                               running mean in registers, no radiance buffer   */
 int  bdpt_last_kernel_features(const bdpt_ctx *ctx);
 /* The black-surface exit rule (BDPT_FEAT_ZERO_EXIT): 1 if ending a path at a black non-emitter is
  * provably exact for this scene -- every term the reference adds after the black hit is finite,
