@@ -420,10 +420,10 @@ def main():
     sched = g.PassScheduler()
     sched.light()
     per_step = wl["passes"] * (units if (wl["scaling"] == "weak" and not wl["fixed_bands"]) else 1)
-    # the auto stream mode measures its candidates on the first eight calls (bdpt.h
+    # the auto stream mode measures its candidates on the first ten calls (bdpt.h
     # bdpt_set_streams): untimed extra steps when --warmup is shorter, so the timed steps run the
     # kernel it settled on
-    tune = max(0, 9 - args.warmup) if args.streams == 0 else 0
+    tune = max(0, 11 - args.warmup) if args.streams == 0 else 0
     # torchrun ranks: one more untimed step after every rank has taken rank 0's choice
     follow = 1 if (args.streams == 0 and world > 1) else 0
     untimed = tune + args.warmup + follow

@@ -119,20 +119,21 @@ struct bdpt_ctx {
     // Four passes per lane: cornell_glass / cornell_mirror +1.2 %, synthetic64 -2.8 % at 128-pass
     // launches, profiles/r03_s45_ab_passes_per_lane.txt -- so it is measured, not fixed.)
     static constexpr double kTuneMargin = 0.05;
-    static constexpr int kTunePhases = 8;
+    static constexpr int kTunePhases = 10;
     bool tune_enabled = true;
     int tune_phase = 0;
     bool tune_fused = false;
     bool tune_pair = true;              // the fused variant kept: paired segment loads or not
     bool tune_quarter = false;          // the pass-stream variant kept: four passes per lane
     bool tune_pool = false;             // the pass-stream variant kept: pixel pools
-    long long tune_call[kTunePhases] = {-1, -1, -1, -1, -1, -1, -1, -1};
-    double tune_ms[kTunePhases] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    bool tune_units = false;            // the pass-stream variant kept: the ordered in-kernel fold
+    long long tune_call[kTunePhases] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+    double tune_ms[kTunePhases] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
     // whether each tuning call really ran its role's variant: four passes per lane needs launches
     // of >= 8 passes, and the unpaired fused variant exists only as a specialised (JIT) build --
     // otherwise the role repeated another role's kernel and must not decide anything
-    bool tune_real[kTunePhases] = {false, false, false, false, false, false, false, false};
-    int tune_npass[kTunePhases] = {0, 0, 0, 0, 0, 0, 0, 0};
+    bool tune_real[kTunePhases] = {false, false, false, false, false, false, false, false, false, false};
+    int tune_npass[kTunePhases] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     // multi-device groups: the peers follow the stream mode devices[0] measured (its decision is
     // copied when they reach the decision point), so every device of a group runs the same kernels
     bdpt_ctx* tune_leader = nullptr;
@@ -577,6 +578,7 @@ static void pool_shape(long nloc, int* R, int* G) {
 // nullptr = use the precompiled instance (reason in c->jit_err).
 // Pass streams with the ordered fold inside the kernel (bdpt_kernels.hip BDPT_UNITS): BDPT_UNITS=P
 // forces it with ranges of P passes (experiments; 0 = never).
+static constexpr int kUnitPasses = 8;   // passes per unit range in the auto mode (profiles/r05_s5_*)
 static int units_env() {
     const char* e = getenv("BDPT_UNITS");
     if (!e || !*e) return -1;
@@ -945,12 +947,14 @@ int bdpt_last_streams(const bdpt_ctx* c) { return c ? c->last_streams : BDPT_EIN
 static int choice_of(const bdpt_ctx* c) {
     if (c->streams_req != 0 || !c->tune_enabled || c->tune_phase != bdpt_ctx::kTunePhases + 1) return 0;
     return BDPT_CHOICE_DECIDED | (c->tune_fused ? BDPT_CHOICE_FUSED : 0) | (c->tune_pair ? BDPT_CHOICE_PAIRED : 0) |
-           (c->tune_quarter ? BDPT_CHOICE_QUARTER : 0) | (c->tune_pool ? BDPT_CHOICE_POOLS : 0);
+           (c->tune_quarter ? BDPT_CHOICE_QUARTER : 0) | (c->tune_pool ? BDPT_CHOICE_POOLS : 0) |
+           (c->tune_units ? BDPT_CHOICE_UNITS : 0);
 }
 
 static int one_set_stream_choice(bdpt_ctx* c, int choice) {
     if (!c) return BDPT_EINVAL;
-    if (!(choice & BDPT_CHOICE_DECIDED) || (choice & ~0x1f))
+    if (!(choice & BDPT_CHOICE_DECIDED) || (choice & ~0x3f) ||
+        ((choice & BDPT_CHOICE_POOLS) && (choice & BDPT_CHOICE_UNITS)))
         return fail(c, BDPT_EINVAL, "bdpt_set_stream_choice: bad choice 0x%x", choice);
     if (c->streams_req != 0)
         return fail(c, BDPT_ESTATE, "bdpt_set_stream_choice: the stream mode is not auto (%d)", c->streams_req);
@@ -958,6 +962,7 @@ static int one_set_stream_choice(bdpt_ctx* c, int choice) {
     c->tune_pair = (choice & BDPT_CHOICE_PAIRED) != 0;
     c->tune_quarter = (choice & BDPT_CHOICE_QUARTER) != 0;
     c->tune_pool = (choice & BDPT_CHOICE_POOLS) != 0;
+    c->tune_units = (choice & BDPT_CHOICE_UNITS) != 0;
     c->tune_enabled = true;
     c->tune_phase = bdpt_ctx::kTunePhases + 1;
     return BDPT_OK;
@@ -1151,6 +1156,7 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
             c->tune_pair = lead->tune_pair;
             c->tune_quarter = lead->tune_quarter;
             c->tune_pool = lead->tune_pool;
+            c->tune_units = lead->tune_units;
             c->tune_phase = bdpt_ctx::kTunePhases + 1;
         }
         if (c->tune_phase == bdpt_ctx::kTunePhases) {        // waits for the last measured call
@@ -1158,13 +1164,15 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
             const double inf = std::numeric_limits<double>::infinity();
             auto per = [&](int r) { return c->tune_real[r] ? c->tune_ms[r] / c->tune_npass[r] : inf; };
             const double half = std::min(per(0), per(3)), quarter = std::min(per(2), per(5));
-            const double pooled = std::min(per(6), per(7));
+            const double pooled = std::min(per(6), per(7)), units = std::min(per(8), per(9));
             const double fp = per(1), fn = per(4);
             c->tune_pair = !(fn < fp);                       // the default unless unpaired was measured faster
             c->tune_quarter = quarter < half;
-            c->tune_pool = pooled < std::min(half, quarter);
+            c->tune_pool = pooled < std::min(half, quarter) && !(units < pooled);
+            c->tune_units = units < std::min(std::min(half, quarter), pooled);
             const double fused = c->tune_pair ? fp : fn;
-            c->tune_fused = fused * (1.0 + bdpt_ctx::kTuneMargin) < std::min(std::min(half, quarter), pooled);
+            const double streams = std::min(std::min(std::min(half, quarter), pooled), units);
+            c->tune_fused = fused * (1.0 + bdpt_ctx::kTuneMargin) < streams;
             c->tune_phase = bdpt_ctx::kTunePhases + 1;
         }
         if (c->tune_phase < bdpt_ctx::kTunePhases && npass >= 2) {
@@ -1215,13 +1223,21 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
     const int penv = pool_env();
     const bool want_pool = !bvh && S > 1 && penv != 0 &&
                            (penv > 0 || (c->streams_req == 0 &&
-                                         (tune_role >= 6 || (tune_role < 0 && c->tune_phase == bdpt_ctx::kTunePhases + 1 &&
-                                                             c->tune_pool))));
+                                         (tune_role == 6 || tune_role == 7 ||
+                                          (tune_role < 0 && c->tune_phase == bdpt_ctx::kTunePhases + 1 &&
+                                           c->tune_pool))));
     if (want_pool) S = chunk < npass ? chunk : npass;        // one pass per lane slice
     // ordered in-kernel fold (units of a tile and a range of passes; no radiance buffer): forced by
-    // BDPT_UNITS=P (ranges of P passes)
+    // BDPT_UNITS=P (ranges of P passes), or measured (tuning roles 8, 9) and kept; not for shards
+    // whose tile workgroups cannot keep the chip busy with one range per tile (a tile's units run
+    // one after another)
     const int uenv = units_env();
-    const bool want_units = !bvh && S > 1 && !want_pool && uenv > 0;
+    const bool units_fit = (long)((c->W + BDPT_BTW - 1) / BDPT_BTW) * grid_rows >= 2L * c->cus * 6;
+    const bool want_units = !bvh && S > 1 && !want_pool && uenv != 0 &&
+                            (uenv > 0 || (c->streams_req == 0 && units_fit &&
+                                          (tune_role >= 8 || (tune_role < 0 && c->tune_phase == bdpt_ctx::kTunePhases + 1 &&
+                                                              c->tune_units))));
+    const int unit_passes = uenv > 0 ? uenv : kUnitPasses;
     c->last_streams = S;
     const int kidx = bvh ? 17 : (a.n <= 16 ? (int)a.n : 0);
     if (bvh) {
@@ -1259,7 +1275,7 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
     }
     // resolve the specialised kernels (a compile on first use) before the timed region starts
     hipFunction_t jf_streams = nullptr, jf_fused = nullptr, jf_pool = nullptr, jf_units = nullptr;
-    bool any_fused = false, pool_ran = false;
+    bool any_fused = false, pool_ran = false, units_ran = false;
     for (int p0 = 0; grid_rows > 0 && p0 < npass; p0 += chunk) {
         const int np = npass - p0 < chunk ? npass - p0 : chunk;
         const bool st = (S < np ? S : np) > 1;
@@ -1298,7 +1314,7 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
         const bool pooled = st && jf_pool != nullptr;        // its pixel-pool build
         const bool unitsl = st && jf_units != nullptr;       // its ordered in-kernel fold build
         a.streams = S < a.npass ? S : a.npass;
-        if (unitsl) a.unit_passes = uenv < a.npass ? uenv : a.npass;
+        if (unitsl) a.unit_passes = unit_passes < a.npass ? unit_passes : a.npass;
         // a workgroup stages the VLPs and sids of its own passes only (bdpt_kernels.hip nslot)
         const size_t slots = unitsl ? (size_t)a.unit_passes : ((size_t)a.npass + a.streams - 1) / a.streams;
         size_t smem = sizeof(float4) * (tab + 3 * slots + 5 + 4 * 128 * 2)
@@ -1381,6 +1397,7 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
             a.gy = grid_rows;
             pgrid = dim3((unsigned)(wgs * nranges), 1, 1);
             c->units_check = true;
+            units_ran = true;
         }
         HIPCHK(c, hipEventRecord(cs.kev[2 * launches], c->stream));
         if (jf)
@@ -1411,7 +1428,8 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
     if (tune_role >= 0) {
         c->tune_real[tune_role] = tune_role == 2 || tune_role == 5 ? quarter_ran
                                   : tune_role == 1 || tune_role == 4 ? (jf_fused != nullptr || tune_role == 1)
-                                  : tune_role >= 6 ? pool_ran
+                                  : tune_role == 6 || tune_role == 7 ? pool_ran
+                                  : tune_role >= 8 ? units_ran
                                   : true;
         c->tune_call[tune_role] = c->issued;
         c->tune_npass[tune_role] = npass;

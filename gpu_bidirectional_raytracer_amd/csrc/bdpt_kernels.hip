@@ -366,6 +366,9 @@ __device__ __forceinline__ f3 cosine_tail(f3 w, f3 u, float u_phi, float u_r2, f
 #ifndef BDPT_UNITS
 #define BDPT_UNITS 0
 #endif
+#ifndef BDPT_UNITS_LDS
+#define BDPT_UNITS_LDS 0
+#endif
 #ifndef BDPT_POOL_FDIV
 #define BDPT_POOL_FDIV 1
 #endif
@@ -964,19 +967,30 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
 
     f3 col = mk(0.f, 0.f, 0.f);
     unsigned cnt0 = 0;                // the counter before pass p is cnt0 + p
+#if BDPT_UNITS_LDS
+    __shared__ float ucol[3][256];
+#endif
     // (units: the counter before the unit's slot k is cnt0 + k)
     const unsigned uflag = kUnits ? (unsigned)vtile * 4u + (unsigned)wave : 0u;   // this wave's 8x8 tile
     if constexpr (kUnits) {
         // the previous range of this tile has folded its passes (in-order WG dispatch makes that a
         // short or no wait); colours and counter are read at the coherence point (agent-scope
         // relaxed atomics: the previous unit may have run on another XCD, whose L2 is not ours)
+#ifndef BDPT_UNITS_NOWAIT
         if (urange > 0) unit_wait(a.unit_flags + uflag, a.unit_tag | urange, a.unit_err);
+#endif
         if (active) {
             col.x = ld_coherent(&a.colors[i].x);
             col.y = ld_coherent(&a.colors[i].y);
             col.z = ld_coherent(&a.colors[i].z);
             cnt0 = __hip_atomic_load(&a.counter[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+#if BDPT_UNITS_LDS
+        // the running mean in LDS instead of three registers live across the path loop
+        ucol[0][threadIdx.x] = col.x;
+        ucol[1][threadIdx.x] = col.y;
+        ucol[2][threadIdx.x] = col.z;
+#endif
     } else if (active) {
         if constexpr (!STREAMS) {
             const bdpt_dev_vec cv = a.colors[i];
@@ -1605,7 +1619,13 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
             if (!done && ++depth > 6) done = true;                       // :621 7-segment cap
             if (done) {                                                  // :774-787
                 if constexpr (!STREAMS || kUnits) {
+#if BDPT_UNITS_LDS
+                    if constexpr (kUnits) col = mk(ucol[0][threadIdx.x], ucol[1][threadIdx.x], ucol[2][threadIdx.x]);
+#endif
                     const unsigned cnt = cnt0 + (unsigned)k;      // S == 1: pass k
+#ifdef BDPT_ABL_NOFOLD
+                    if (__float_as_uint(rad.x) != 0x7fc00123u) {} else   // ablation: no running mean
+#endif
                     if (cnt == 0) {
                         col = rad;
                     } else {
@@ -1615,6 +1635,13 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                         col.y = (col.y * k1 + rad.y) * k2;
                         col.z = (col.z * k1 + rad.z) * k2;
                     }
+#if BDPT_UNITS_LDS
+                    if constexpr (kUnits) {
+                        ucol[0][threadIdx.x] = col.x;
+                        ucol[1][threadIdx.x] = col.y;
+                        ucol[2][threadIdx.x] = col.z;
+                    }
+#endif
                 } else {
                     bdpt_dev_vec r;
                     r.x = rad.x; r.y = rad.y; r.z = rad.z;
@@ -1755,15 +1782,22 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
     }
 #endif
     if constexpr (kUnits) {
+#if BDPT_UNITS_LDS
+        col = mk(ucol[0][threadIdx.x], ucol[1][threadIdx.x], ucol[2][threadIdx.x]);
+#endif
         // the unit's result, then this wave tile's flag: the next range's unit may start
         if (active && k > 0) {
             st_coherent(&a.colors[i].x, col.x);
             st_coherent(&a.colors[i].y, col.y);
             st_coherent(&a.colors[i].z, col.z);
             __hip_atomic_store(&a.counter[i], cnt0 + (unsigned)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            a.pixels[i] = bdpt_dev_to_rgba(col.x, col.y, col.z, a.gamma_thr);
         }
+        // pixels once, by the launch's last range: plain stores of several units (on several XCDs,
+        // each with its own write-back L2) would reach memory in no defined order
+        if (active && s0 + nslot >= a.npass) a.pixels[i] = bdpt_dev_to_rgba(col.x, col.y, col.z, a.gamma_thr);
+#ifndef BDPT_UNITS_NOEND
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");          // the stores above are performed
+#endif
         if (lane == 0)
             __hip_atomic_store(a.unit_flags + uflag, a.unit_tag | (urange + 1u), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);

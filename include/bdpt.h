@@ -97,13 +97,16 @@ int  bdpt_set_shard(bdpt_ctx *ctx, int shard, int nshards, int band_rows);
 /* Pass streams (no reference counterpart; results are bit-identical for every S): S lanes per
  * pixel render passes s, s+S, ... into an HBM radiance buffer (12 B per pass and pixel) and an
  * ordered fold applies the running mean of device.cu:774-787 in pass order.
- *   0  = auto (default): the first eight calls of >= 2 passes measure, in this order, the
+ *   0  = auto (default): the first ten calls of >= 2 passes measure, in this order, the
  *        pass-stream kernel with two passes per lane (S = ceil(passes / 2); one per lane in
  *        launches of < 4 passes or with the BVH), the fused kernel with paired segment loads,
  *        pass streams with four passes per lane (S = ceil(passes / 4), launches of >= 8), two
- *        per lane again, the fused kernel without pairing, four per lane again, and twice pass
+ *        per lane again, the fused kernel without pairing, four per lane again, twice pass
  *        streams with pixel pools (S = passes, lanes restart on new pixels of their pass;
- *        specialised builds, BDPT_FEAT_POOLS); later calls use the pass-stream variant with the
+ *        specialised builds, BDPT_FEAT_POOLS), and twice the ordered in-kernel fold (units of a
+ *        tile and 8 passes, running mean in registers, no radiance buffer and no fold kernel;
+ *        specialised builds of frames with >= 2 x CUs x 6 tile workgroups, BDPT_FEAT_UNITS);
+ *        later calls use the pass-stream variant with the
  *        fastest call, or the faster fused variant if its time per pass (path kernels + a quarter of the fold) beat that by 5 %
  *        (closed scenes with long paths favour pass streams, open scenes with short paths the
  *        fused kernel or pools); re-measured after a scene / shard / traversal change;
@@ -126,6 +129,7 @@ int  bdpt_last_streams(const bdpt_ctx *ctx);
 #define BDPT_CHOICE_PAIRED  4               /* the fused variant with paired segment loads    */
 #define BDPT_CHOICE_QUARTER 8               /* pass streams with four passes per lane         */
 #define BDPT_CHOICE_POOLS  16               /* pass streams with pixel pools                  */
+#define BDPT_CHOICE_UNITS  32               /* pass streams with the ordered in-kernel fold   */
 int  bdpt_stream_choice(const bdpt_ctx *ctx);
 int  bdpt_set_stream_choice(bdpt_ctx *ctx, int choice);
 /* Device k of a (multi-device) context (0 = devices[0]): S and BDPT_FEAT_* bits of its last

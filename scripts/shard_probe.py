@@ -2,7 +2,7 @@
 
 For each N, the first and last rank's share of an N-way band shard (1/N of the rows; N x passes
 for weak scaling, the same passes with --strong) is rendered on one GPU with auto pass streams
-(after the auto mode's eight measured calls) and with the S values asked for, and its device time
+(after the auto mode's ten measured calls) and with the S values asked for, and its device time
 is compared with the N = 1 step: efficiency = t(N=1) / t(rank share), over N for --strong, with t
 the wall time of back-to-back asynchronous calls between two synchronisations (as bench.py times its steps:
 a pass-stream call's fold overlaps the next call's path kernel); the device ms of the calls
@@ -32,7 +32,7 @@ import gpu_bidirectional_raytracer_amd as g  # noqa: E402
 from gpu_bidirectional_raytracer_amd import sharding as shd  # noqa: E402
 
 
-WARM = 9
+WARM = 11
 
 
 def run(sp, cam, W, H, sid, vlp, shard, nshards, band, streams, reps):
@@ -41,7 +41,7 @@ def run(sp, cam, W, H, sid, vlp, shard, nshards, band, streams, reps):
     r.set_streams(streams)
     r.light_pass(0)
     n = len(sid) // (reps + WARM)
-    for k in range(WARM):                               # warm-up (the auto mode measures 6 calls)
+    for k in range(WARM):                               # warm-up (the auto mode measures 10 calls)
         r.path_passes(sid[k * n:(k + 1) * n], vlp[k * n:(k + 1) * n], sync=False)
     r.synchronize()
     r.path_timing(reset=True)

@@ -124,11 +124,11 @@ def test_group_devices_follow_devices0_stream_choice(gpu):
     W, H = 321, 241
     cam, sp = g.read_scene(os.path.join(SCENES, "caustic.scn"))
     g.update_camera(cam, W, H)
-    sid, vlp = schedule(16 * 10)
+    sid, vlp = schedule(16 * 12)
     with g.Renderer(sp, W, H, cam, devices=[gpu, gpu, gpu]) as r:
         r.set_streams(0)
         r.light_pass(0)
-        for k in range(10):                                       # 8 measured calls, then the choice
+        for k in range(12):                                       # 10 measured calls, then the choice
             r.path_passes(sid[16 * k:16 * (k + 1)], vlp[16 * k:16 * (k + 1)])
         modes = [r.device_mode(k) for k in range(3)]
         assert "decided" in modes[0]["choice"]

@@ -204,38 +204,62 @@ def test_per_lane_streams_policy(gpu):
 
 @pytest.mark.parametrize("name", ["cornell", "caustic"])
 def test_auto_streams_measured(gpu, rnd0, name):
-    """Auto (0): the first eight calls of >= 2 passes run pass streams with two passes per lane
+    """Auto (0): the first ten calls of >= 2 passes run pass streams with two passes per lane
     (launches of >= 4 passes), the fused kernel with paired segment loads, pass streams with four
     passes per lane (launches of >= 8), two per lane again, the fused kernel without pairing,
-    four per lane again, and twice pass streams with pixel pools (one pass per lane slice, S =
-    the call's passes); later calls use the fastest pass-stream variant, or the faster fused one
-    if it measured faster still; a scene change measures again.  Every call's result is the
-    oracle's whatever was chosen."""
+    four per lane again, twice pass streams with pixel pools (one pass per lane slice, S = the
+    call's passes), and twice the ordered in-kernel fold (units; frames too small for it -- this
+    one -- repeat two passes per lane there, and those calls decide nothing); later calls use the
+    fastest pass-stream variant, or the faster fused one if it measured faster still; a scene
+    change measures again.  Every call's result is the oracle's whatever was chosen."""
     W, H = 97, 65
     r, cam, sp = make(name, W, H, gpu)
-    sid, vlp = schedule(96)
+    sid, vlp = schedule(112)
     r.path_passes(sid[:1], vlp[:1])                        # 1 pass: not a measurement
     assert r.last_streams == 1
-    for k, want in enumerate((4, 1, 2, 4, 1, 2, 8, 8)):   # the eight measured calls of 8 passes
+    for k, want in enumerate((4, 1, 2, 4, 1, 2, 8, 8, 4, 4)):   # the ten measured calls of 8 passes
         a0 = 1 + 8 * k
         r.path_passes(sid[a0:a0 + 8], vlp[a0:a0 + 8])
         assert r.last_streams == want, (k, r.last_streams)
-        if k >= 6:
+        if k in (6, 7):
             assert "pixel_pools" in r.last_features, (k, r.last_features)
+        assert "unit_fold" not in r.last_features, (k, r.last_features)
     used = []
-    for a0 in (65, 73):
+    for a0 in (81, 89):
         r.path_passes(sid[a0:a0 + 8], vlp[a0:a0 + 8])
         used.append(r.last_streams)
     assert used[0] == used[1] and used[0] in (1, 2, 4, 8), used
+    assert "decided" in r.device_mode(0)["choice"] and "units" not in r.device_mode(0)["choice"]
     col, cnt = r.read_radiance()
     lp = oracle.light_pass(sp, rnd0, 0)
-    ocol, ocnt, opix = oracle.path_passes(sp, rnd0, cam, W, H, lp, sid[:81], vlp[:81])
+    ocol, ocnt, opix = oracle.path_passes(sp, rnd0, cam, W, H, lp, sid[:97], vlp[:97])
     assert_same(cnt, ocnt, "counter")
     assert_same(col, ocol, "colors")
     assert_same(r.read_pixels(), opix, "pixels")
     r.set_scene(sp)                                        # ReInitScene: measure again
-    r.path_passes(sid[81:88], vlp[81:88])
+    r.path_passes(sid[97:104], vlp[97:104])
     assert r.last_streams == 4                             # 7 passes, two per lane
+    r.close()
+
+
+def test_auto_streams_measure_units(gpu, rnd0):
+    """A frame with enough tile workgroups (1025 x 769: 33 x 97 = 3,201 >= 2 x CUs x 6): the
+    ninth and tenth measured calls run the ordered in-kernel fold (units); every call's frame is
+    still the oracle's (checked on a band of rows)."""
+    W, H = 1025, 769
+    r, cam, sp = make("cornell", W, H, gpu)
+    sid, vlp = schedule(8 * 12)
+    for k in range(12):
+        r.path_passes(sid[8 * k:8 * (k + 1)], vlp[8 * k:8 * (k + 1)])
+        if k in (8, 9):
+            assert "unit_fold" in r.last_features, (k, r.last_features)
+    col, cnt = r.read_radiance()
+    assert (cnt == 96).all()
+    lp = oracle.light_pass(sp, rnd0, 0)
+    for y0 in (0, 384, 760):
+        ocol, ocnt, opix = oracle.path_passes(sp, rnd0, cam, W, H, lp, sid, vlp, rows=(y0, y0 + 2))
+        assert_same(col[y0:y0 + 2], ocol[y0:y0 + 2], f"colors rows {y0}")
+        assert_same(r.read_pixels()[y0:y0 + 2], opix[y0:y0 + 2], f"pixels rows {y0}")
     r.close()
 
 
