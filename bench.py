@@ -301,19 +301,38 @@ def smt_yield(scene, W, H, y0, sid, vlp, seconds, usable):
             "node_physical_cores": len(set(topo.values())) or None}
 
 
-def _pmc_record(name, workload, scene, W, H, passes_per_launch, streams, specialized):
-    """The PMC record of profiles/<name> for this exact configuration (files hold one record per
-    workload and pass-stream count, keyed workload@S<streams>), or None."""
+def kernel_kind(features, streams):
+    """Which path kernel a run used: "units" (ordered in-kernel fold), "pools" (pass streams with
+    pixel pools), "fused" (S = 1) or "streams" (pass streams; then S matters too)."""
+    if "unit_fold" in features:
+        return "units"
+    if "pixel_pools" in features:
+        return "pools"
+    return "fused" if streams == 1 else "streams"
+
+
+def pmc_key(workload, kind, streams):
+    """Record key of profiles/pmc_*.json: workload@<kind>, plus S<streams> for plain pass streams."""
+    return f"{workload}@{kind}" + (f"S{streams}" if kind == "streams" else "")
+
+
+def _pmc_record(name, workload, scene, W, H, passes_per_launch, streams, specialized, kind=None):
+    """The PMC record of profiles/<name> for this exact configuration (one record per workload
+    and kernel, keyed pmc_key), or None.  Records without a "kernel" field (round 4 and before)
+    are plain pass streams, or the fused kernel at S = 1."""
     path = os.path.join(REPO, "profiles", name)
     if not os.path.exists(path):
         return None
     data = json.load(open(path))
     recs = data.values() if isinstance(data, dict) and "scene" not in data else [data]
+    kind = kind or ("fused" if streams == 1 else "streams")
     for rec in recs:
+        rkind = rec.get("kernel") or ("fused" if rec.get("pass_streams") == 1 else "streams")
         if rec.get("workload", "cornell1080") == workload and rec.get("scene") == scene \
                 and rec.get("width") == W and rec.get("height") == H \
                 and float(rec.get("passes_per_launch", -1)) == float(passes_per_launch) \
-                and rec.get("pass_streams") == streams and bool(rec.get("specialized", False)) == bool(specialized):
+                and rkind == kind and (kind != "streams" or rec.get("pass_streams") == streams) \
+                and bool(rec.get("specialized", False)) == bool(specialized):
             return rec
     return None
 
@@ -610,7 +629,12 @@ def main():
         roofline = None
         if w is not None:
             samples_per_launch = own_pixels * passes_per_launch
-            if r.last_streams > 1:
+            if "unit_fold" in features:
+                # ordered in-kernel fold: colors + counter read and written once per unit of
+                # kUnitPasses (8) passes, pixels once per launch; no radiance buffer
+                units = max(1.0, passes_per_launch / 8)
+                bytes_per_launch = own_pixels * (32 * units + 4) + samples_per_launch * 4 * w["rng_reads"]
+            elif r.last_streams > 1:
                 # pass streams: the path kernel reads the counter once and writes 12 B of radiance
                 # per sample; the fold kernel (not this launch) does the colors/pixels RMW
                 bytes_per_launch = own_pixels * 4 + samples_per_launch * (4 * w["rng_reads"] + 12)
@@ -619,8 +643,9 @@ def main():
             gbs = bytes_per_launch / avg_launch_s / 1e9
             fl = flop_per_sample(w) * samples_per_launch / avg_launch_s / 1e12
             single = world == 1 and ndev == 1
+            kind = kernel_kind(features, r.last_streams)
             trec = _pmc_record("pmc_traffic.json", args.workload, wl["scene"], W, H, passes_per_launch,
-                               r.last_streams, r.last_specialized) if single else None
+                               r.last_streams, r.last_specialized, kind) if single else None
             skips = [f for f in features if f in ("det_skip", "zero_exit", "last_skip", "bvh")]
             roofline = {"bound": "valu", "achieved": round(fl, 3), "peak": FP32_NOFMA_TFLOPS, "unit": "TFLOP/s",
                         "frac": round(fl / FP32_NOFMA_TFLOPS, 4),
@@ -647,7 +672,7 @@ def main():
                                      "valu_issue_occupancy_pmc (the instruction mix priced at measured gfx950 issue costs, "
                                      "DESIGN.md section 10)")
             vrec = _pmc_record("pmc_valu.json", args.workload, wl["scene"], W, H, passes_per_launch,
-                               r.last_streams, r.last_specialized) if single else None
+                               r.last_streams, r.last_specialized, kind) if single else None
             if vrec:
                 for k in ("valu_busy", "valu_lane_utilisation", "wait_frac", "issue_stall_frac", "active_frac",
                           "valu_insts_per_wave", "l2_hit_rate", "valu_issue_occupancy"):

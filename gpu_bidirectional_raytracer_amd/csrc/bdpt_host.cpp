@@ -45,20 +45,7 @@ extern "C" __global__ void bdpt_light_kernel(const bdpt_dev_sphere*, unsigned, c
 extern "C" const void* bdpt_path_kernel_table[36];   // [(S > 1) * 18 + (BVH ? 17 : n <= 16 ? n : 0)]
 extern "C" __global__ void bdpt_pixels_kernel(const bdpt_dev_vec*, uchar4*, const float*, int);
 extern "C" __global__ void bdpt_accum_kernel(bdpt_path_args);
-extern "C" __global__ void bdpt_accum_nt_kernel(bdpt_path_args);
-extern "C" __global__ void bdpt_accum_nt8_kernel(bdpt_path_args);
-extern "C" __global__ void bdpt_accum_u8_kernel(bdpt_path_args);
-// the fold kernel (BDPT_FOLD_KIND = nt | nt8 | u8: experiments)
-static const void* fold_kernel() {
-    static const void* k = [] {
-        const char* e = getenv("BDPT_FOLD_KIND");
-        if (e && !strcmp(e, "nt")) return (const void*)&bdpt_accum_nt_kernel;
-        if (e && !strcmp(e, "nt8")) return (const void*)&bdpt_accum_nt8_kernel;
-        if (e && !strcmp(e, "u8")) return (const void*)&bdpt_accum_u8_kernel;
-        return (const void*)&bdpt_accum_kernel;
-    }();
-    return k;
-}
+
 extern "C" __global__ void bdpt_frame_add_kernel(float*, const float*, unsigned*, const unsigned*, int);
 
 // gamma thresholds (host, once): see bdpt_util.c
@@ -605,20 +592,6 @@ static hipFunction_t jit_path_kernel_build(bdpt_ctx* c, bool streams, bool pair,
         geom += (i ? ",{" : "{") + hexf(sp.p.x) + "," + hexf(sp.p.y) + "," + hexf(sp.p.z) + "," + hexf(rr) + "}";
     }
     geom += "}";
-    // the emitters' NEE records, formed exactly as upload_scene forms d_lightrec
-    std::string lrec = "{";
-    int nl = 0;
-    for (unsigned i = 0; i < n; i++) {
-        const bdpt_sphere& sp = c->spheres[i];
-        if (sp.e.x == 0.f && sp.e.y == 0.f && sp.e.z == 0.f) continue;
-        const float kPi = 3.14159265358979323846f;
-        const float area = 4.f * kPi * sp.rad * sp.rad;
-        lrec += std::string(nl ? "," : "") + "{" + hexf(sp.p.x) + "," + hexf(sp.p.y) + "," + hexf(sp.p.z) + "," +
-                hexf(sp.rad) + "},{" + hexf(sp.e.x) + "," + hexf(sp.e.y) + "," + hexf(sp.e.z) + "," + hexf(area) + "}";
-        nl++;
-    }
-    if (nl == 0) lrec += "{0,0,0,0},{0,0,0,0}";
-    lrec += "}";
     // Black-surface exit (bdpt_kernels.hip BDPT_ZERO_EXIT): compiled in only when ending a path at
     // a black non-emitter is provably exact for this scene (bdpt_util.c bdpt_zero_exit_safe).
     const bool zero_exit = bdpt_zero_exit_safe(c->spheres.data(), n) != 0;
@@ -636,7 +609,6 @@ static hipFunction_t jit_path_kernel_build(bdpt_ctx* c, bool streams, bool pair,
             "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize",
             "-fno-gpu-flush-denormals-to-zero", "-DBDPT_JIT=1", "-DBDPT_JIT_N=" + std::to_string(n),
             "-DBDPT_JIT_EMIS=" + std::to_string(emis) + "ull", "-DBDPT_JIT_GEOM=" + geom,
-            "-DBDPT_JIT_NL=" + std::to_string(nl), "-DBDPT_JIT_LREC=" + lrec,
             "-DBDPT_JIT_ZERO_SAFE=" + std::to_string(zero_exit ? 1 : 0),
             "-DBDPT_WAVES_PER_SIMD=" + std::to_string(waves)};
         std::vector<std::string> all = opts;
@@ -1410,9 +1382,7 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
             grid.z = 1;
             HIPCHK(c, hipEventRecord(c->rb_path_ev[half], c->stream));
             HIPCHK(c, hipStreamWaitEvent(c->fstream, c->rb_path_ev[half], 0));
-            static const bool abl_nofold = getenv("BDPT_ABL_NOFOLD") != nullptr;   // ablation
-            if (!abl_nofold)
-                HIPCHK(c, hipLaunchKernel(fold_kernel(), grid, block, kargs, 0, c->fstream));
+            HIPCHK(c, hipLaunchKernel((const void*)&bdpt_accum_kernel, grid, block, kargs, 0, c->fstream));
             HIPCHK(c, hipEventRecord(c->rb_fold_ev[half], c->fstream));
             c->rb_used[half] = true;
             c->fold_last = half;

@@ -23,15 +23,6 @@
 struct jit_geom { float x, y, z, w; };
 constexpr jit_geom kJitGeom[BDPT_JIT_N] = BDPT_JIT_GEOM;
 constexpr unsigned long long kJitEmis = BDPT_JIT_EMIS;
-// the emitters' NEE records {p, rad}, {e, (4*pi*rad)*rad} (bdpt_host.cpp upload_scene), folded too
-// Folding the NEE records too (BDPT_JIT_LIGHTS=1) frees 8 VGPRs (71: 7 waves/SIMD, 64 without
-// spills at 8) but the compiler then issues 2.5 % more VALU instructions, and every occupancy from
-// 5 to 8 waves/SIMD measured the same: cornell -1 to -2 %, so it is off by default.
-#ifndef BDPT_JIT_LIGHTS
-#define BDPT_JIT_LIGHTS 0
-#endif
-constexpr int kJitNL = BDPT_JIT_NL;
-constexpr jit_geom kJitLrec[2 * (BDPT_JIT_NL > 0 ? BDPT_JIT_NL : 1)] = BDPT_JIT_LREC;
 #endif
 
 namespace {
@@ -49,9 +40,6 @@ __device__ __forceinline__ float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y 
 // [2^-125, 2^125) (all 2^32 inputs checked on gfx950 by tests/native/hw_exact_check.hip); other
 // x take the library division on an exec-masked branch.  rcp_rn_inrange: caller proves the range.
 __device__ __forceinline__ float rcp_rn_inrange(float x) {
-#ifdef BDPT_LIB_DIV
-    return 1.f / x;
-#endif
     const float r = __builtin_amdgcn_rcpf(x);
     return __builtin_fmaf(__builtin_fmaf(-x, r, 1.f), r, r);
 }
@@ -83,23 +71,9 @@ __device__ __forceinline__ float div_rn_normal(float a, float b) {
     const float r = __builtin_fmaf(-q, b, a);
     return __builtin_fmaf(r, y, q);
 }
-#ifndef BDPT_DIV_MARKSTEIN
-#define BDPT_DIV_MARKSTEIN 1
-#endif
-
-#ifndef BDPT_NORM1
-#define BDPT_NORM1 1
-#endif
 __device__ __forceinline__ f3 norm(f3 v) {
-#ifdef BDPT_ABL_DIV
-    return smul(__builtin_amdgcn_rsqf(dot(v, v)), v);
-#endif
-#if BDPT_NORM1
     float root;
     return smul(rcp_sqrt_rn(dot(v, v), &root), v);             // one range test (above)
-#else
-    float l = rcp_rn(bdpt_sqrt_rn(dot(v, v))); return smul(l, v);
-#endif
 }
 __device__ __forceinline__ f3 cross(f3 a, f3 b) {
     return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
@@ -115,19 +89,13 @@ __device__ const double bdpt_sincos_table_dev[BDPT_SC_N][2] = BDPT_SINCOS_TABLE_
 
 // sinf/cosf with correctly-rounded semantics: fp64 sincos rounded once to fp32 (bdpt_math.h),
 // table-driven when the caller has the sin(2pi k/N) table in LDS.
-#ifndef BDPT_SINCOS_TABLE
-#define BDPT_SINCOS_TABLE 1
-#endif
 // The choice is a template argument, not a null test on `tab`: the compiler cannot prove an
 // LDS-derived pointer non-null, and the dead minimax path then kept its fp64 coefficients in
 // ~20 VGPRs across the whole path loop.
 template <bool TAB>
 __device__ __forceinline__ void sincos_cr(float x, float* s, float* c, const double* tab) {
-#ifdef BDPT_ABL_SINCOS
-    *s = __sinf(x); *c = __cosf(x); return;
-#endif
     double sd, cd;
-    if constexpr (TAB && BDPT_SINCOS_TABLE) bdpt_sincos_tab((double)x, tab, &sd, &cd);
+    if constexpr (TAB) bdpt_sincos_tab((double)x, tab, &sd, &cd);
     else bdpt_sincos_dp((double)x, &sd, &cd);
     *s = (float)sd;
     *c = (float)cd;
@@ -147,31 +115,18 @@ __device__ __forceinline__ float sphere_isect(float4 g, f3 o, f3 d) {
     return det < 0.f ? 0.f : r;
 }
 
-// The same test with "no hit" encoded as +inf instead of 0, so the closest-hit update is one
-// compare (d < t) and the any-hit test is d < maxt.  t1 > EPS ? t1 : (t2 > EPS ? t2 : miss) ==
-// (r = t1 > EPS ? t1 : t2) > EPS ? r : miss.
+// The two roots of the same test, t1 <= t2 (fl is monotone and the root is >= 0; both NaN for a
+// negative det).  With r = t1 > EPS ? t1 : t2, the reference's hit (t1 > EPS ? t1 : t2 > EPS ?
+// t2 : miss) is "r if t2 > EPS": when t1 > EPS, t2 >= t1 > EPS too.  So the closest-hit update is
+// `t2 > EPS && r < t` and the shadow test `t2 > EPS && r < maxt`: one select fewer than with a
+// +inf miss encoding (two compares and a select instead of two selects and a compare).
 // The reference's `det < 0 -> miss` needs no test of its own (+2.7 % measured): a negative normal
-// det gives a NaN root (bdpt_sqrt_rn_core), so t1, t2, r are NaN and r > EPS fails; so does a
+// det gives a NaN root (bdpt_sqrt_rn_core), so t1, t2, r are NaN and t2 > EPS fails; so does a
 // generated NaN det.  A negative denormal det may give a root of -0 (v_sqrt_f32 flushes it), so
 // r = b -- but then b <= EPS, a miss again: if b > EPS, then fl(b*b) >= 1e-4 and X = fl(b*b - oo)
 // is either > 0 (oo < b*b/2; then det >= X > 0) or a multiple of 2^-38 (ulp(oo) >= 2^-38), and
 // det = fl(X + r*r) is then >= 0, <= -2^-39, or a nonzero multiple of ulp(r*r) >= 2^-83 -- never
 // in (-2^-126, 0).  (det is never -0: fl(b*b) is not -0.)
-__device__ __forceinline__ float sphere_isect_inf(float4 g, f3 o, f3 d) {
-    f3 op = mk(g.x - o.x, g.y - o.y, g.z - o.z);
-    float b = dot(op, d);
-    float det = b * b - dot(op, op) + g.w;
-    const float s = bdpt_sqrt_rn_core(det);
-    const float t1 = b - s, t2 = b + s;
-    const float r = t1 > kEps ? t1 : t2;
-    return r > kEps ? r : __builtin_inff();
-}
-
-// The two roots of the same test, t1 <= t2 (fl is monotone and the root is >= 0; both NaN for a
-// negative det).  With r = t1 > EPS ? t1 : t2, the reference's hit (t1 > EPS ? t1 : t2 > EPS ?
-// t2 : miss) is "r if t2 > EPS": when t1 > EPS, t2 >= t1 > EPS too.  So the closest-hit update is
-// `t2 > EPS && r < t` and the shadow test `t2 > EPS && r < maxt`: one select fewer than with the
-// +inf miss encoding (two compares and a select instead of two selects and a compare).
 struct troots { float t1, t2; };
 __device__ __forceinline__ troots sphere_roots(float4 g, f3 o, f3 d) {
     f3 op = mk(g.x - o.x, g.y - o.y, g.z - o.z);
@@ -180,9 +135,6 @@ __device__ __forceinline__ troots sphere_roots(float4 g, f3 o, f3 d) {
     const float s = bdpt_sqrt_rn_core(det);
     return {b - s, b + s};
 }
-#ifndef BDPT_T2VALID
-#define BDPT_T2VALID 1
-#endif
 // The same test in two steps, so that a wave can stop after `det` when no lane's det is >= 0 (or
 // NaN): every such lane misses (the reference returns 0 for det < 0, device.cu:95), so the root,
 // its correction, the two roots and the selects of that sphere are skipped for the whole wave.
@@ -218,35 +170,17 @@ __device__ __forceinline__ troots roots_of(tdet q) {
 #define BDPT_IKEY 0
 #endif
 #endif
-#ifndef BDPT_IKEY_ASM
-#define BDPT_IKEY_ASM 1
-#endif
 constexpr unsigned kKeyC = 0x3C23D70Bu;                      // bits(0.01f) + 1
 __device__ __forceinline__ unsigned key_of(float x) { return __float_as_uint(x) - kKeyC; }
 __device__ __forceinline__ unsigned umin2(unsigned a, unsigned b) { return a < b ? a : b; }
-// one v_min3_u32 (left to itself the compiler compares min(b, c) with a and keeps a separate min)
+// one v_min3_u32 (left to itself the compiler compares min(b, c) with a and keeps a separate min:
+// two half-rate v_min_u32, and the kernels ran 0.5-1 % slower than without keys)
 __device__ __forceinline__ unsigned umin3(unsigned a, unsigned b, unsigned c) {
-#if BDPT_IKEY_ASM
     unsigned r;
     asm("v_min3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
     return r;
-#else
-    return umin2(a, umin2(b, c));
-#endif
 }
 __device__ __forceinline__ unsigned maxt_key(float maxt) { return maxt > kEps ? key_of(maxt) : 0u; }
-#ifndef BDPT_DET_SKIP
-#define BDPT_DET_SKIP 1
-#endif
-#ifndef BDPT_ZERO_EXIT
-#define BDPT_ZERO_EXIT 1
-#endif
-#ifndef BDPT_LAST_SKIP
-#define BDPT_LAST_SKIP 1
-#endif
-#ifndef BDPT_NEE_MARKSTEIN
-#define BDPT_NEE_MARKSTEIN 1
-#endif
 
 // UniformSampleSphereDevice device.cu:157-165
 template <bool TAB = false>
@@ -296,12 +230,6 @@ __device__ __forceinline__ f3 cosine_tail(f3 w, f3 u, float u_phi, float u_r2, f
     return add(nd, w);
 }
 
-#ifndef BDPT_MERGE_REFR
-#define BDPT_MERGE_REFR 1
-#endif
-#ifndef BDPT_PACK_EDGES
-#define BDPT_PACK_EDGES 1
-#endif
 // Fused S = 1 kernel: a lane whose path ends parks until at least BDPT_REGEN_K lanes of its wave
 // (or all of its live lanes) are parked; then they start their next passes together, so the
 // camera-ray and path-start code runs for groups of lanes instead of a few lanes in almost every
@@ -316,9 +244,6 @@ __device__ __forceinline__ f3 cosine_tail(f3 w, f3 u, float u_phi, float u_r2, f
 // group restarts on one slot, so one sid and depth).  Two passes per lane with grouping against
 // one pass per lane, one-session A/B (profiles/r03_s16_ab_regen_streams.txt): cornell +0.7 %,
 // cornell_glass +0.8 %, synthetic64 -0.2 %; without grouping two passes per lane cost 3.5-6 %.
-#ifndef BDPT_REGEN_STREAMS
-#define BDPT_REGEN_STREAMS 1
-#endif
 // Fused kernel: a parking lane loads its next pass's first-segment randoms at once (it waits at
 // least an iteration before it uses them), and its camera randoms a second time into cr0, cr1
 // (buffer loads, so the compiler does not merge them with the q0, q1 loads).  caustic8 +1.9 %,
@@ -326,9 +251,6 @@ __device__ __forceinline__ f3 cosine_tail(f3 w, f3 u, float u_phi, float u_r2, f
 // loading at release (cornell -1.1 % with it).  An ablation without any table reads runs caustic8
 // 37 % faster: the fused kernel's random gathers (20 B per lane and segment at unrelated
 // addresses, 6.6 TB/s of L2 fills) are what is left to win on open scenes.
-#ifndef BDPT_PARK_PREFETCH
-#define BDPT_PARK_PREFETCH 1
-#endif
 // Fused kernel: the randoms of two segments (depth d even and d + 1) are loaded together, so a
 // path's table line is fetched once for both instead of being evicted from L2 between them
 // (caustic8 +9 %, open -4 %: the auto stream mode measures the fused kernel with and without it
@@ -337,17 +259,8 @@ __device__ __forceinline__ f3 cosine_tail(f3 w, f3 u, float u_phi, float u_r2, f
 #define BDPT_RNG_PAIR 1
 #endif
 // pass streams: radiance stores to the fold buffer with the nontemporal (streaming) hint
-#ifndef BDPT_RBUF_NT
-#define BDPT_RBUF_NT 0
-#endif
 // pass streams: parked lanes load their next pass's randoms at park time (see the loop)
-#ifndef BDPT_PARK_LOAD
-#define BDPT_PARK_LOAD 1
-#endif
 // pass streams: the segment's randoms settled before the radiance stores (see the loop)
-#ifndef BDPT_Q_SETTLED
-#define BDPT_Q_SETTLED 1
-#endif
 // Pass streams with pixel pools (a build with BDPT_POOL; bdpt_host.cpp launches it with a.pool = R):
 // a wave renders ONE pass, and a lane whose path ends takes the next pixel of the wave's pool --
 // the lanes stay on one sid, so a restarted group's random gathers stay adjacent in the planar
@@ -366,20 +279,8 @@ __device__ __forceinline__ f3 cosine_tail(f3 w, f3 u, float u_phi, float u_r2, f
 #ifndef BDPT_UNITS
 #define BDPT_UNITS 0
 #endif
-#ifndef BDPT_UNITS_LDS
-#define BDPT_UNITS_LDS 0
-#endif
-#ifndef BDPT_POOL_FDIV
-#define BDPT_POOL_FDIV 1
-#endif
 // paired loads: the odd-depth copy of the paired randoms at the point of use (see the loop)
-#ifndef BDPT_PAIR_AT_USE
-#define BDPT_PAIR_AT_USE 1
-#endif
 // camera terms: per-lane fp64 base in LDS, kz products formed once per workgroup
-#ifndef BDPT_CAMB
-#define BDPT_CAMB 1
-#endif
 
 }  // namespace
 
@@ -548,20 +449,11 @@ __device__ __forceinline__ float4 ld_const(const float4* p, int i) {
 // a hash of j instead -- the cost of the table reads.
 __device__ __forceinline__ void load_rand5(const float* __restrict__ rnd, unsigned j, float& q0,
                                            float& q1, float& q2, float& q3, float& q4) {
-#if defined(BDPT_ABL_RNG)
-    auto h = [](unsigned v) { v *= 2654435761u; v ^= v >> 15; return ((v >> 8) | 1u) * 0x1p-24f; };
-    q0 = h(j); q1 = h(j + 1); q2 = h(j + 2); q3 = h(j + 3); q4 = h(j + 4);
-#elif defined(BDPT_RAND_X4)
-    typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
-    const f4u v = *(const f4u*)(rnd + j);
-    q0 = v.x; q1 = v.y; q2 = v.z; q3 = v.w; q4 = rnd[j + 4];
-#else
     q0 = rnd[j]; q1 = rnd[j + 1]; q2 = rnd[j + 2]; q3 = rnd[j + 3]; q4 = rnd[j + 4];
-#endif
 }
 
 // The same five entries through a buffer descriptor with one 32-bit offset register (the fused
-// kernel, BDPT_RNG_BUF): no 64-bit address temporaries, which the register allocator otherwise
+// kernel): no 64-bit address temporaries, which the register allocator otherwise
 // took from registers a pending load writes -- and then waited for that load right after issuing it.
 __device__ __forceinline__ void load_rand5b(__amdgpu_buffer_rsrc_t rs, unsigned j, float& q0,
                                             float& q1, float& q2, float& q3, float& q4) {
@@ -571,13 +463,7 @@ __device__ __forceinline__ void load_rand5b(__amdgpu_buffer_rsrc_t rs, unsigned 
     q0 = __uint_as_float(v.x); q1 = __uint_as_float(v.y); q2 = __uint_as_float(v.z); q3 = __uint_as_float(v.w);
     q4 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, vo, 16, 0));
 }
-#ifndef BDPT_RNG_BUF
-#define BDPT_RNG_BUF 1
-#endif
 
-#ifndef BDPT_RAND_PLANAR
-#define BDPT_RAND_PLANAR 1
-#endif
 // d_Rand[j .. j+4] from the planar copy: plane j mod 25 + c at j / 25, as buffer loads with the
 // plane offsets c * PL in the scalar offset (one address register for all five)
 __device__ __forceinline__ void load_rand5p(__amdgpu_buffer_rsrc_t rs, unsigned j, float& q0,
@@ -696,14 +582,6 @@ extern "C" int bdpt_debug_stats(unsigned long long* out, int reset) {
 #ifndef BDPT_WAVES_PER_SIMD
 #define BDPT_WAVES_PER_SIMD 5
 #endif
-// Part-full shadow rounds split the sphere list over lane groups (path kernel, shadow queue).
-#ifndef BDPT_SPLIT_TAIL
-#define BDPT_SPLIT_TAIL 1
-#endif
-// Shadow rays of full rounds: occlusion kept as a wave lane mask with a uniform exit
-#ifndef BDPT_ANYHIT_MASK
-#define BDPT_ANYHIT_MASK 1
-#endif
 // (the specialised build is compiled with -DBDPT_WAVES_PER_SIMD=6: folding the scene in frees
 // registers, and 6 waves/SIMD measured +3 % over 5 on cornell)
 // BVH scenes: 5 waves/SIMD too, although the traversal state spills 10 VGPRs at 96 (measured:
@@ -723,11 +601,7 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
     constexpr bool kBVH = N < 0;      // large scene: walls brute force + BVH (bdpt_bvh.cpp)
     const int n = N > 0 ? N : (int)a.n;
     constexpr int kUnroll = N > 0 ? N : 1;
-#ifdef BDPT_BVH_LDS
-    constexpr bool kTreeLds = true;   // tree copied to LDS per workgroup (3 per CU)
-#else
     constexpr bool kTreeLds = false;  // tree read through L1/L2: 4 workgroups per CU (+10 %)
-#endif
     const int ntree = kTreeLds ? 2 * a.bvh_nn + a.bvh_ns : 0;
     const int ntab = kBVH ? ntree + a.big_n : 4 * n;
     // pass stream: this workgroup's lanes render passes s0, s0+S, s0+2S, ... (slots k = 0, 1, ...)
@@ -807,12 +681,8 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
     if (threadIdx.x == 0) {
         K[0] = make_float4(a.ux[0], a.ux[1], a.ux[2], a.tx);
         K[1] = make_float4(a.uy[0], a.uy[1], a.uy[2], a.ty);
-#if BDPT_CAMB
         // kz * ud and tz * kz (kz = 10, device.cu:583-590): the same products, formed once
         K[2] = make_float4(10.0f * a.ud[0], 10.0f * a.ud[1], 10.0f * a.ud[2], a.tz * 10.0f);
-#else
-        K[2] = make_float4(a.ud[0], a.ud[1], a.ud[2], a.tz);
-#endif
         K[3] = make_float4(a.orig[0], a.orig[1], a.orig[2], 0.f);
         K[4] = make_float4(a.inv_w, a.inv_h, 0.f, 0.f);
     }
@@ -843,7 +713,7 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
         if constexpr (N > 0) return (a.emis_mask >> s) & 1u;
         else return (__float_as_int(C[s].w) & 256) != 0;
     };
-    // spheres worth a wave-uniform det test (BDPT_DET_SKIP): non-walls of a specialised kernel
+    // spheres worth a wave-uniform det test: non-walls of a specialised kernel
     auto small_sphere = [&](int s) -> bool {
 #ifdef BDPT_JIT
         if constexpr (N == BDPT_JIT_N) return kJitGeom[s].w < 1e6f;
@@ -868,7 +738,6 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
 #endif
     int x = vbx * BDPT_BTW + (wave % BDPT_BLOCK_WX) * BDPT_WTW + (lane % BDPT_WTW);
     int ly = vby * BDPT_BTH + (wave / BDPT_BLOCK_WX) * BDPT_WTH + (lane / BDPT_WTW);
-#if BDPT_PACK_EDGES
     // Frame edges packed into full waves (rows not remapped to shard bands): a frame whose width
     // leaves tw <= 8 columns in the last workgroup column (1921 = 60 x 32 + 1) would give every
     // tile row one wave with tw x 8 live lanes that still runs whole paths; instead those tw x H
@@ -889,7 +758,6 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
             ly = yt + q / xt;
         }
     }
-#endif
     const int yoff = (bdpt_dev_tile_row(a, vby) - vby) * BDPT_BTH;   // uniform
     int y = ly + yoff;
     bool active = x < a.W && y < a.H;
@@ -924,14 +792,9 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
         if (q >= pend) return false;
         // q / W through the fp32 reciprocal (q < 2^28, W < 2^16: the estimate is off by at most
         // one row) and one correction, instead of an integer division
-#if BDPT_POOL_FDIV
         int lr = (int)((float)q * __builtin_amdgcn_rcpf((float)a.W));
         px = (int)q - lr * a.W;
         if (px < 0) { lr--; px += a.W; } else if (px >= a.W) { lr++; px -= a.W; }
-#else
-        const int lr = (int)(q / (unsigned)a.W);
-        px = (int)q - lr * a.W;
-#endif
         py = bdpt_dev_tile_row(a, lr / BDPT_BTH) * BDPT_BTH + lr % BDPT_BTH;
         if (py >= a.H) return false;
         return a.nshards <= 1 || a.tiles_per_band > 0 || ((py / a.band_rows) % a.nshards) == a.shard;
@@ -948,13 +811,11 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
     // Pass p = s0 + k*S (slot k) is rendered iff counter0 + p < 30000 (one increment per pass).
     float4* SQ = Q + wave * kQueue * 2;
 
-#if BDPT_CAMB
     // this lane's camera terms ((double)((float)x * iw) - iw*W/2., same for y) of device.cu:565-566,
     // formed once per launch instead of once per pass
     __shared__ double2 camb[256];
     camb[threadIdx.x] = make_double2((double)((float)x * a.inv_w) - a.half_w,
                                      (double)((float)y * a.inv_h) - a.half_h);
-#endif
     const int i = active ? y * a.W + x : 0;
     const unsigned ibase = 26u + (unsigned)(i * 25);
     // The pixel coordinates live in one packed register (W, H < 2^16, bdpt_create) and are
@@ -967,30 +828,19 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
 
     f3 col = mk(0.f, 0.f, 0.f);
     unsigned cnt0 = 0;                // the counter before pass p is cnt0 + p
-#if BDPT_UNITS_LDS
-    __shared__ float ucol[3][256];
-#endif
     // (units: the counter before the unit's slot k is cnt0 + k)
     const unsigned uflag = kUnits ? (unsigned)vtile * 4u + (unsigned)wave : 0u;   // this wave's 8x8 tile
     if constexpr (kUnits) {
         // the previous range of this tile has folded its passes (in-order WG dispatch makes that a
         // short or no wait); colours and counter are read at the coherence point (agent-scope
         // relaxed atomics: the previous unit may have run on another XCD, whose L2 is not ours)
-#ifndef BDPT_UNITS_NOWAIT
         if (urange > 0) unit_wait(a.unit_flags + uflag, a.unit_tag | urange, a.unit_err);
-#endif
         if (active) {
             col.x = ld_coherent(&a.colors[i].x);
             col.y = ld_coherent(&a.colors[i].y);
             col.z = ld_coherent(&a.colors[i].z);
             cnt0 = __hip_atomic_load(&a.counter[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-#if BDPT_UNITS_LDS
-        // the running mean in LDS instead of three registers live across the path loop
-        ucol[0][threadIdx.x] = col.x;
-        ucol[1][threadIdx.x] = col.y;
-        ucol[2][threadIdx.x] = col.z;
-#endif
     } else if (active) {
         if constexpr (!STREAMS) {
             const bdpt_dev_vec cv = a.colors[i];
@@ -1003,18 +853,17 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
     unsigned depth = 0;
     unsigned j = (ibase + SID[k]) % M5;
     float q0, q1, q2, q3, q4;
-#if BDPT_RAND_PLANAR
     // one pass per lane (pass streams, S = npass): the lanes of a wave stay on one sid and depth,
     // so their gathers are adjacent in the planar copy (wave-uniform choice)
     // (the fused kernel keeps the linear table: its lanes are on different passes and depths, and
     // planar reads measured -57 % on caustic8, -38 % with whole-wave lockstep groups)
-    const bool planar = STREAMS && (nslot == 1 || BDPT_REGEN_STREAMS) && a.rndp != nullptr;
-    constexpr bool kRegen = BDPT_REGEN_K > 1 && (!STREAMS || BDPT_REGEN_STREAMS);
-    constexpr bool kParkPf = kRegen && BDPT_PARK_PREFETCH && !STREAMS;
+    const bool planar = STREAMS && a.rndp != nullptr;
+    constexpr bool kRegen = BDPT_REGEN_K > 1;
+    constexpr bool kParkPf = kRegen && !STREAMS;
     // pass streams: a parked lane loads its next pass's first randoms when it parks, with the
     // other lanes' prefetch (loading them at the release instead wrote registers the continuing
     // lanes' prefetch had just targeted, and the compiler waited for that prefetch first)
-    constexpr bool kParkLoad = kRegen && BDPT_PARK_LOAD && STREAMS;
+    constexpr bool kParkLoad = kRegen && STREAMS;
     float cr0 = 0.f, cr1 = 0.f;                     // camera randoms of a released lane (kParkPf)
     // (read through a buffer descriptor: the compiler would otherwise merge them with the q0, q1
     // loads of the same addresses and copy them over behind a vmcnt(0))
@@ -1024,18 +873,15 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
         cr0 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsl, jc * 4u, 0, 0));
         cr1 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsl, jc * 4u, 4, 0));
     };
-    // the linear table: plain loads (pass streams) or buffer loads (fused kernel, BDPT_RNG_BUF)
+    // the linear table: plain loads (pass streams) or buffer loads (fused kernel)
     auto load_lin = [&](unsigned jj, float& a0, float& a1, float& a2, float& a3, float& a4) {
-#if BDPT_RNG_BUF && !defined(BDPT_ABL_RNG)
         if constexpr (!STREAMS) { load_rand5b(rsl, jj, a0, a1, a2, a3, a4); return; }
-#endif
         load_rand5(rnd, jj, a0, a1, a2, a3, a4);
     };
     const __amdgpu_buffer_rsrc_t rsp = __builtin_amdgcn_make_buffer_rsrc(
         (void*)a.rndp, (short)0, (int)(BDPT_DEV_RANDP_PLANES * BDPT_DEV_RANDP_PL * 4u), 0x00020000);
     if (planar) load_rand5p(rsp, j, q0, q1, q2, q3, q4);
     else
-#endif
     load_lin(j, q0, q1, q2, q3, q4);
     // BDPT_RNG_PAIR: n0..n4 = the next segment's randoms, loaded with q0..q4 at even depths
     constexpr bool kPair = !STREAMS && BDPT_RNG_PAIR;
@@ -1067,7 +913,6 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
         if (alive) {
             if (fresh) {                  // camera ray (:562-600); d_Rand[kk] == q0 (kk == j)
                 const float4 c0 = K[0], c1 = K[1], c2 = K[2], c3 = K[3], k4 = K[4];
-#if BDPT_CAMB
                 // device.cu:565-566: ((float)x*iw - iw*W/2.) + d_Rand[kk]*iw in fp64, then fp32
                 const double2 cb = camb[threadIdx.x];
                 const float u0 = kParkPf ? cr0 : q0, u1 = kParkPf ? cr1 : q1;
@@ -1078,20 +923,6 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                 rdir = add(rdir, smul(ky, mk(c1.x, c1.y, c1.z)));
                 rdir = add(rdir, mk(c2.x, c2.y, c2.z));                       // kz * ud
                 const float w = (c0.w * kx + c1.w * ky + c2.w) + 1;           // c2.w = tz * kz
-#else
-                unsigned xyv = xy;
-                asm volatile("" : "+v"(xyv));
-                const int x = (int)(xyv & 0xffffu), y = (int)(xyv >> 16);
-                // device.cu:565-566: ((float)x*iw - iw*W/2.) + d_Rand[kk]*iw in fp64, then fp32
-                const float kx = (float)(((double)((float)x * k4.x) - a.half_w) + (double)(q0 * k4.x));
-                const float ky = (float)(((double)((float)y * k4.y) - a.half_h) + (double)(q1 * k4.y));
-                const float kz = 10.0f;
-                f3 rdir = mk(0.f, 0.f, 0.f);
-                rdir = add(rdir, smul(kx, mk(c0.x, c0.y, c0.z)));
-                rdir = add(rdir, smul(ky, mk(c1.x, c1.y, c1.z)));
-                rdir = add(rdir, smul(kz, mk(c2.x, c2.y, c2.z)));
-                const float w = (c0.w * kx + c1.w * ky + c2.w * kz) + 1;
-#endif
                 // (float)(1./(double)w) == 1.f/w: double rounding of a quotient is innocuous
                 // when 53 >= 2*24 + 2 (device.cu:594)
                 rdir = smul(rcp_rn(w), rdir);
@@ -1134,31 +965,26 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                     }
                 }
             } else {
-#if BDPT_T2VALID && BDPT_DET_SKIP && defined(BDPT_JIT)
+#ifdef BDPT_JIT
                 if constexpr (N == BDPT_JIT_N) {
-#if BDPT_IKEY
+                    // specialised kernels: integer keys (one v_min3_u32 per sphere) and the
+                    // wave-uniform det skip for the non-wall spheres
                     unsigned kt = key_of(t);
-#endif
                     auto hit = [&](int s) -> bool {
                         const tdet qd = sphere_det(geom(s), ro, rd);
                         if (small_sphere(s) && __builtin_amdgcn_ballot_w64(!(qd.det < 0.f)) == 0)
                             return true;                          // every lane misses sphere s
                         const troots q = roots_of(qd);
-#if BDPT_IKEY
                         const unsigned nk = umin3(kt, key_of(q.t1), key_of(q.t2));
                         id = nk < kt ? s : id;
                         kt = nk;
-#else
-                        const float r = q.t1 > kEps ? q.t1 : q.t2;
-                        if (q.t2 > kEps && r < t) { t = r; id = s; }
-#endif
                         return true;
                     };
                     unroll_down<N - 1>(hit);
-#if BDPT_IKEY
                     t = __uint_as_float(kt + kKeyC);
+                } else
 #endif
-                } else {
+                {
 #pragma unroll kUnroll
                     for (int s = n - 1; s >= 0; --s) {
                         const troots q = sphere_roots(geom(s), ro, rd);
@@ -1166,25 +992,10 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                         if (q.t2 > kEps && r < t) { t = r; id = s; }
                     }
                 }
-#elif BDPT_T2VALID
-#pragma unroll kUnroll
-                for (int s = n - 1; s >= 0; --s) {
-                    const troots q = sphere_roots(geom(s), ro, rd);
-                    const float r = q.t1 > kEps ? q.t1 : q.t2;
-                    if (q.t2 > kEps && r < t) { t = r; id = s; }
-                }
-#else
-#pragma unroll kUnroll
-                for (int s = n - 1; s >= 0; --s) {
-                    const float d = sphere_isect_inf(geom(s), ro, rd);
-                    if (d < t) { t = d; id = s; }
-                }
-#endif
             }
             done = id < 0;
         }
         BDPT_TICK(0);                 // camera ray + closest hit
-#if BDPT_PAIR_AT_USE
         // paired loads: an odd-depth segment takes the randoms loaded with the previous one --
         // here, after the closest hit and just before the shading uses them, not where the next
         // loads are issued: a copy there made the compiler merge the loaded values through
@@ -1194,7 +1005,6 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
         if constexpr (kPair) {
             if (alive && (depth & 1u)) { q0 = n0; q1 = n1; q2 = n2; q3 = n3; q4 = n4; }
         }
-#endif
         if (alive) {
             if (!done) {
                 const float4 cm = tabC(id);
@@ -1210,7 +1020,7 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                         rad = add(rad, mul(thr, smul(fabsf(dp), mk(em.x, em.y, em.z))));
                     }
                     done = true;
-#if BDPT_ZERO_EXIT && defined(BDPT_JIT) && BDPT_JIT_ZERO_SAFE
+#if defined(BDPT_JIT) && BDPT_JIT_ZERO_SAFE
                 } else if (N == BDPT_JIT_N && (mat & 512)) {
                     // A black surface (cornell's front wall) makes the throughput exactly 0 (the
                     // reference multiplies it by c = 0 whatever the material), so everything the
@@ -1219,7 +1029,6 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                     // >= 1 from every other surface, bdpt_host.cpp).  rad is final: end the path.
                     done = true;
 #endif
-#if BDPT_MERGE_REFR
                 } else {
                     // DIFF (:663-703), SPEC (:704-714), REFR (:715-770).  Nearly every wave holds
                     // a few refracting lanes next to its diffuse ones, so the diffuse and the
@@ -1229,7 +1038,6 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                     // per lane, so the results are unchanged.
                     const bool isdiff = (mat & 255) == BDPT_DEV_DIFF;
                     const f3 cc = mk(cm.x, cm.y, cm.z);
-#if BDPT_LAST_SKIP
                     // the path's last segment (depth 6, :621): the next direction and the
                     // specular weights are never used -- a diffuse vertex still weights its NEE
                     if (depth >= 6u) {
@@ -1239,7 +1047,6 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                             diff = true;
                         }
                     } else {
-#endif
                     f3 refl = rd;
                     bool refr = false, into = false;
                     float nnt = 0.f, ddn = 0.f, cos2t = 0.f;
@@ -1289,68 +1096,14 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                             const float Tr = 1.f - Re;
                             const float Pp = .25f + .5f * Re;
                             const bool reflect = q2 < Pp;
-#if BDPT_DIV_MARKSTEIN
                             const float k = div_rn_normal(reflect ? Re : Tr, reflect ? Pp : 1.f - Pp);
-#else
-                            const float k = (reflect ? Re : Tr) / (reflect ? Pp : 1.f - Pp);
-#endif
                             thr = mul(smul(k, thr), cc);
                             rd = reflect ? refl : U;
                         }
                     }
-#if BDPT_LAST_SKIP
-                    }
-#endif
-                    ro = hit;
-                }
-#else
-                } else if ((mat & 255) == BDPT_DEV_DIFF) {               // :663-703
-                    specular = false;
-                    thr = mul(thr, mk(cm.x, cm.y, cm.z));
-                    diff = true;                  // shadow rays: below, compacted over the wave
-                    ro = hit;
-                    rd = cosine_dir<true>(nl, q0, q1, SCT);
-                } else {
-                    // SPEC :704-714 and REFR / LITE :715-770 share the mirror direction (one
-                    // evaluation when a wave holds lanes of both kinds)
-                    specular = true;
-                    const f3 refl = sub(rd, smul(2.f * dot(normal, rd), normal));
-                    if ((mat & 255) == BDPT_DEV_SPEC) {
-                        thr = mul(thr, mk(cm.x, cm.y, cm.z));
-                        rd = refl;
-                    } else {
-                        const bool into = dot(normal, nl) > 0;
-                        const float nc = 1.f, nt = 1.5f;
-                        const float nnt = into ? nc / nt : nt / nc;
-                        const float ddn = dot(rd, nl);
-                        const float cos2t = 1.f - nnt * nnt * (1.f - ddn * ddn);
-                        if (cos2t < 0.f) {
-                            thr = mul(thr, mk(cm.x, cm.y, cm.z));
-                            rd = refl;
-                        } else {
-                            // cos2t = 1 - X is 0 or >= 2^-24 (Sterbenz for X >= 1/2, else > 1/2)
-                            const float kq = (float)(into ? 1 : -1) * (ddn * nnt + bdpt_sqrt_rn_core(cos2t));
-                            const f3 td = norm(sub(smul(nnt, rd), smul(kq, normal)));
-                            const float aa = nt - nc, bb = nt + nc;
-                            const float R0 = aa * aa / (bb * bb);
-                            const float c = 1 - (into ? -ddn : dot(td, normal));
-                            const float Re = R0 + (1 - R0) * c * c * c * c * c;
-                            const float Tr = 1.f - Re;
-                            const float Pp = .25f + .5f * Re;
-                            // RP = Re / P or TP = Tr / (1 - P): only the one the lane uses is divided
-                            const bool reflect = q2 < Pp;
-#if BDPT_DIV_MARKSTEIN
-                            const float k = div_rn_normal(reflect ? Re : Tr, reflect ? Pp : 1.f - Pp);
-#else
-                            const float k = (reflect ? Re : Tr) / (reflect ? Pp : 1.f - Pp);
-#endif
-                            thr = mul(smul(k, thr), mk(cm.x, cm.y, cm.z));
-                            rd = reflect ? refl : td;
-                        }
                     }
                     ro = hit;
                 }
-#endif
             }
         }
 
@@ -1360,20 +1113,11 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
         if (__builtin_amdgcn_ballot_w64(diff) != 0) {
             f3 res = mk(0.f, 0.f, 0.f), usp = res, vsd = res, vcon = res;
             if (diff) usp = uniform_sphere<true>(q3, q4, SCT);
-#if defined(BDPT_JIT) && BDPT_JIT_LIGHTS
-            const int nlights = N == BDPT_JIT_N ? kJitNL : (int)a.n_lights;
-#else
             const int nlights = (int)a.n_lights;
-#endif
-            auto lrec = [&](int k) -> float4 {
-#if defined(BDPT_JIT) && BDPT_JIT_LIGHTS
-                if constexpr (N == BDPT_JIT_N) {
-                    const jit_geom g = kJitLrec[k];
-                    return make_float4(g.x, g.y, g.z, g.w);
-                }
-#endif
-                return ld_const(a.lightrec, k);
-            };
+            // the emitters' NEE records {p, rad}, {e, (4*pi*rad)*rad} (bdpt_host.cpp upload_scene)
+            // through the constant address space (folding them into the specialised build freed
+            // 8 VGPRs but issued 2.5 % more VALU instructions: cornell -1 to -2 % at 5..8 waves)
+            auto lrec = [&](int k) -> float4 { return ld_const(a.lightrec, k); };
             const int nsteps = nlights > 0 ? nlights : 1;
             for (int li = 0; li < nsteps; li++) {                         // uniform
                 bool has_nee = false, has_vlp = false;
@@ -1394,7 +1138,6 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                             has_nee = true;
                             maxt = len - kEps;
                             const float na = le.w * wi * wo, nb = len * len;
-#if BDPT_NEE_MARKSTEIN
                             // one Markstein step (div_rn_normal) when a, b lie in [2^-60, 2^60]:
                             // then 1/b, a/b and the residual stay normal; otherwise (grazing
                             // wi * wo) the library division on an exec-masked branch
@@ -1404,9 +1147,6 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                                 kq = div_rn_normal(na, nb);
                             else
                                 kq = na / nb;
-#else
-                            const float kq = na / nb;
-#endif
                             con = smul(kq, mk(le.x, le.y, le.z));
                         }
                     }
@@ -1460,7 +1200,6 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                 }
 #endif
                 for (int base = 0; base < total; base += 64) {            // uniform
-#if BDPT_SPLIT_TAIL
                     // A part-full round (<= 32 rays; typically the second round, ~14 rays for
                     // cornell) is traced by 2^lg lane groups that split the sphere list: ray r
                     // goes to lanes r, r + 64/2^lg, ...; group g tests spheres n-1-g, n-1-g-2^lg,
@@ -1483,16 +1222,12 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                                 const unsigned km = maxt_key(r0.w);
 #endif
                                 for (int s = n - 1 - g; s >= 0; s -= 1 << lg) {
+                                    const troots q = sphere_roots(G[s], o, d);
 #if BDPT_IKEY
-                                    const troots q = sphere_roots(G[s], o, d);
                                     if (umin2(key_of(q.t1), key_of(q.t2)) < km && !(vac && emissive(s))) { occ = 1; break; }
-#elif BDPT_T2VALID
-                                    const troots q = sphere_roots(G[s], o, d);
+#else
                                     const float rr = q.t1 > kEps ? q.t1 : q.t2;
                                     if (q.t2 > kEps && rr < r0.w && !(vac && emissive(s))) { occ = 1; break; }
-#else
-                                    const float dd = sphere_isect_inf(G[s], o, d);
-                                    if (dd < r0.w && !(vac && emissive(s))) { occ = 1; break; }
 #endif
                                 }
                             }
@@ -1502,17 +1237,12 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                             continue;
                         }
                     }
-#endif
                     const int idx = base + lane;
                     if (idx < total) {
                         const float4 r0 = SQ[idx], r1 = SQ[kQueue + idx];
                         const f3 o = mk(r0.x, r0.y, r0.z), d = mk(r1.x, r1.y, r1.z);
                         const bool vac = r1.w != 0.f;
                         unsigned occ = 0;
-#ifdef BDPT_ABL_SHADOW
-                        occ = r0.w < -1e30f || vac;
-                        if (0)
-#endif
                         if constexpr (kBVH) {                             // IntersectP(Vacuum)Device
                             for (int q = 0; q < a.big_n && !occ; q++) {
                                 const troots h = sphere_roots(BG[q], o, d);
@@ -1535,7 +1265,6 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                                 node = occ ? a.bvh_nn : __float_as_int(lo.w);
                             }
                         } else {
-#if BDPT_ANYHIT_MASK
                         // occlusion as a wave lane mask (SGPRs): every lane tests every sphere
                         // until all of the round's rays are occluded (one uniform branch per
                         // sphere).  No per-lane break, so no nest of saved exec masks -- for 64
@@ -1548,10 +1277,8 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                         const unsigned km = maxt_key(r0.w);
 #endif
                         auto step = [&](int s) -> bool {                  // IntersectP(Vacuum)Device
-#if BDPT_T2VALID
                             const tdet qd = sphere_det(geom(s), o, d);
-                            if (BDPT_DET_SKIP && small_sphere(s) &&
-                                __builtin_amdgcn_ballot_w64(!(qd.det < 0.f)) == 0)
+                            if (small_sphere(s) && __builtin_amdgcn_ballot_w64(!(qd.det < 0.f)) == 0)
                                 return true;                          // every ray misses sphere s
                             const troots q = roots_of(qd);
 #if BDPT_IKEY
@@ -1563,10 +1290,6 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                             unsigned long long h = __builtin_amdgcn_ballot_w64(q.t2 > kEps) &
                                                    __builtin_amdgcn_ballot_w64(rr < r0.w);
 #endif
-#else
-                            const float dd = sphere_isect_inf(geom(s), o, d);
-                            unsigned long long h = __builtin_amdgcn_ballot_w64(dd < r0.w);
-#endif
                             if (emissive(s)) h &= ~vacm;
                             occm |= h;
                             return occm != live;
@@ -1576,15 +1299,6 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                         if constexpr (N > 0) unroll_down<N - 1>(step);
                         else for (int s = n - 1; s >= 0 && step(s); --s) {}
                         occ = (unsigned)(occm >> lane) & 1u;
-#else
-#pragma unroll kUnroll
-                        for (int s = n - 1; s >= 0; --s) {                // IntersectP(Vacuum)Device
-                            const float dd = sphere_isect_inf(geom(s), o, d);
-                            // early exit (measured +2% over a branch-free loop, +9% over a
-                            // branch-free running minimum of integer-keyed distances)
-                            if (dd < r0.w && !(vac && emissive(s))) { occ = 1; break; }
-                        }
-#endif
                         }
                         SQ[idx].w = __uint_as_float(occ);
                     }
@@ -1607,25 +1321,17 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
         }
 
         BDPT_TICK(4);                 // shadow results + contribution
-#if BDPT_Q_SETTLED
         // pass streams: the segment's randoms are settled here, before this iteration's radiance
         // stores.  The loads that refill their registers below then have no earlier load of the
         // same registers to wait for -- the compiler otherwise waits for every outstanding memory
         // operation there, the just-issued stores included (their loads completed long before:
         // the shading used them; the wait appeared on paths that skip the shading).
         if constexpr (STREAMS) asm volatile("" ::"v"(q0), "v"(q1), "v"(q2), "v"(q3), "v"(q4));
-#endif
         if (alive) {
             if (!done && ++depth > 6) done = true;                       // :621 7-segment cap
             if (done) {                                                  // :774-787
                 if constexpr (!STREAMS || kUnits) {
-#if BDPT_UNITS_LDS
-                    if constexpr (kUnits) col = mk(ucol[0][threadIdx.x], ucol[1][threadIdx.x], ucol[2][threadIdx.x]);
-#endif
                     const unsigned cnt = cnt0 + (unsigned)k;      // S == 1: pass k
-#ifdef BDPT_ABL_NOFOLD
-                    if (__float_as_uint(rad.x) != 0x7fc00123u) {} else   // ablation: no running mean
-#endif
                     if (cnt == 0) {
                         col = rad;
                     } else {
@@ -1635,34 +1341,15 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                         col.y = (col.y * k1 + rad.y) * k2;
                         col.z = (col.z * k1 + rad.z) * k2;
                     }
-#if BDPT_UNITS_LDS
-                    if constexpr (kUnits) {
-                        ucol[0][threadIdx.x] = col.x;
-                        ucol[1][threadIdx.x] = col.y;
-                        ucol[2][threadIdx.x] = col.z;
-                    }
-#endif
                 } else {
                     bdpt_dev_vec r;
                     r.x = rad.x; r.y = rad.y; r.z = rad.z;
                     unsigned xyv = xy;
                     asm volatile("" : "+v"(xyv));
                     const int li = kPool ? (int)lix : ((int)(xyv >> 16) - yoff) * a.W + (int)(xyv & 0xffffu);
-#ifdef BDPT_ABL_NOFOLD
-                    // ablation (results change): no radiance store -- the fold's upper bound
-                    if (__float_as_uint(rad.x) == 0x7fc00123u)
-#endif
                     {
                     bdpt_dev_vec* rp = a.rbuf + (size_t)(s0 + k * S) * a.nloc + (size_t)li;
-#if BDPT_RBUF_NT
-                    // streaming stores: the radiance is read once, by the fold, long after -- keep
-                    // it from displacing the random table's lines in L2
-                    __builtin_nontemporal_store(r.x, &rp->x);
-                    __builtin_nontemporal_store(r.y, &rp->y);
-                    __builtin_nontemporal_store(r.z, &rp->z);
-#else
                     *rp = r;
-#endif
                     }
                 }
                 fresh = true;
@@ -1686,31 +1373,20 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                 // loop (one LDS read and four integer ops per segment, against a spill; keeping j
                 // live and adding 5 per segment measured 1 % slower)
                 if (kPair && (depth & 1u)) {             // loaded with the previous segment's
-#if !BDPT_PAIR_AT_USE
-                    q0 = n0; q1 = n1; q2 = n2; q3 = n3; q4 = n4;
-#endif
                 } else {
                 unsigned xyv = xy;
                 asm volatile("" : "+v"(xyv));
                 const unsigned li = (xyv >> 16) * (unsigned)a.W + (xyv & 0xffffu);
                 j = (26u + li * 25u + depth * 5u + SID[k]) % M5;
-#if BDPT_RAND_PLANAR
                 if (planar) load_rand5p(rsp, j, q0, q1, q2, q3, q4);
                 else
-#endif
                 {
-#if BDPT_PAIR_AT_USE
                 // the camera randoms first: the camera ray waits for them at the top of the loop,
                 // and the memory counter drains in issue order, so the segment loads issued after
                 // them may stay in flight through the camera ray and the closest hit
                 if (kParkPf && parked) load_cam(j);
                 load_lin(j, q0, q1, q2, q3, q4);
                 if (kPair) load_next(j);
-#else
-                load_rand5(rnd, j, q0, q1, q2, q3, q4);
-                if (kPair) load_next(j);
-                if (kParkPf && parked) load_cam(j);
-#endif
                 }
                 }
             }
@@ -1728,10 +1404,8 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                     want = false;
                     lix = q;
                     xy = ((unsigned)py << 16) | (unsigned)px;
-#if BDPT_CAMB
                     camb[threadIdx.x] = make_double2((double)((float)px * a.inv_w) - a.half_w,
                                                      (double)((float)py * a.inv_h) - a.half_h);
-#endif
                     parked = true;
                 }
                 mw = __builtin_amdgcn_ballot_w64(want);
@@ -1744,10 +1418,8 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                 asm volatile("" : "+v"(xyv));
                 const unsigned li = (xyv >> 16) * (unsigned)a.W + (xyv & 0xffffu);
                 j = (26u + li * 25u + depth * 5u + SID[k]) % M5;
-#if BDPT_RAND_PLANAR
                 if (planar) load_rand5p(rsp, j, q0, q1, q2, q3, q4);
                 else
-#endif
                 load_lin(j, q0, q1, q2, q3, q4);
             }
         }
@@ -1764,10 +1436,8 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                     asm volatile("" : "+v"(xyv));
                     const unsigned li = (xyv >> 16) * (unsigned)a.W + (xyv & 0xffffu);
                     const unsigned jr = (26u + li * 25u + SID[k]) % M5;
-#if BDPT_RAND_PLANAR
                     if (planar) load_rand5p(rsp, jr, q0, q1, q2, q3, q4);
                     else
-#endif
                     load_lin(jr, q0, q1, q2, q3, q4);
                     if (kPair) load_next(jr);
                 }
@@ -1782,9 +1452,6 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
     }
 #endif
     if constexpr (kUnits) {
-#if BDPT_UNITS_LDS
-        col = mk(ucol[0][threadIdx.x], ucol[1][threadIdx.x], ucol[2][threadIdx.x]);
-#endif
         // the unit's result, then this wave tile's flag: the next range's unit may start
         if (active && k > 0) {
             st_coherent(&a.colors[i].x, col.x);
@@ -1795,9 +1462,7 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
         // pixels once, by the launch's last range: plain stores of several units (on several XCDs,
         // each with its own write-back L2) would reach memory in no defined order
         if (active && s0 + nslot >= a.npass) a.pixels[i] = bdpt_dev_to_rgba(col.x, col.y, col.z, a.gamma_thr);
-#ifndef BDPT_UNITS_NOEND
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");          // the stores above are performed
-#endif
         if (lane == 0)
             __hip_atomic_store(a.unit_flags + uflag, a.unit_tag | (urange + 1u), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
@@ -1826,8 +1491,7 @@ extern "C" const void* bdpt_path_kernel_table[36] = {BDPT_ROW(false), BDPT_ROW(t
 // Ordered fold of pass-stream radiance (S > 1): the running mean of device.cu:774-787 applied
 // to rbuf[0..npass) in pass order, so the result is the S == 1 result bit for bit.  Same grid
 // rows (and shard remap) as the path launch; one thread per pixel.
-template <bool NT, int U>
-__device__ __forceinline__ void accum_body(const bdpt_path_args& a) {
+extern "C" __global__ __launch_bounds__(256) void bdpt_accum_kernel(bdpt_path_args a) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #ifdef BDPT_PROF
     // section profile (experiments): shader cycles per wave between wave-uniform points, summed
@@ -1864,40 +1528,14 @@ __device__ __forceinline__ void accum_body(const bdpt_path_args& a) {
         }
         cnt++;
     };
-    // (a version with 8 loads in flight ran faster alone but slowed the overlapped path kernel
-    // of the next launch: caustic8 -1.3 %)
-    auto ld = [&](int p) -> bdpt_dev_vec {
-        const bdpt_dev_vec* q = rb + (size_t)p * a.nloc;
-        if constexpr (NT) {
-            bdpt_dev_vec v;
-            v.x = __builtin_nontemporal_load(&q->x);
-            v.y = __builtin_nontemporal_load(&q->y);
-            v.z = __builtin_nontemporal_load(&q->z);
-            return v;
-        }
-        return *q;
-    };
-    int p = 0;
-    if constexpr (U > 1) {
-        for (; p + U <= n; p += U) {
-            bdpt_dev_vec v[U];
-#pragma unroll
-            for (int u = 0; u < U; u++) v[u] = ld(p + u);
-#pragma unroll
-            for (int u = 0; u < U; u++) fold(v[u]);
-        }
-    }
-    for (; p < n; p++) fold(ld(p));
+    // (folds with 8 loads in flight, or with streaming loads, ran faster alone but slowed the
+    // concurrent path kernel more: caustic8 -1.3 % (round 2), -4 to -13 % (profiles/r05_s3_*))
+    for (int p = 0; p < n; p++) fold(rb[(size_t)p * a.nloc]);
     if (cnt == cnt0) return;
     a.colors[i] = col;
     a.counter[i] = cnt;
     a.pixels[i] = bdpt_dev_to_rgba(col.x, col.y, col.z, a.gamma_thr);
 }
-extern "C" __global__ __launch_bounds__(256) void bdpt_accum_kernel(bdpt_path_args a) { accum_body<false, 1>(a); }
-// fold variants (experiments, BDPT_FOLD_KIND): streaming loads, loads in flight
-extern "C" __global__ __launch_bounds__(256) void bdpt_accum_nt_kernel(bdpt_path_args a) { accum_body<true, 1>(a); }
-extern "C" __global__ __launch_bounds__(256) void bdpt_accum_nt8_kernel(bdpt_path_args a) { accum_body<true, 8>(a); }
-extern "C" __global__ __launch_bounds__(256) void bdpt_accum_u8_kernel(bdpt_path_args a) { accum_body<false, 8>(a); }
 
 // Frame assembly of a multi-device context without RCCL: add a peer's zero-padded frame (exact:
 // each pixel is non-zero on one device only, and x + 0 == x).

@@ -27,12 +27,15 @@ print(f"FETCH (MB) / WRITE (MB)     {g('FETCH_SIZE') / 1024:.1f} / {g('WRITE_SIZ
 # figures plus the bench configuration of the PMC runs, read by bench.py into its `valu` object
 if len(sys.argv) > 4:
     import json
-    cfg, ppl = {}, None
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench  # noqa: E402  (record keys)
+    cfg, ppl, feats = {}, None, []
     for f in sorted(glob.glob(os.path.join(root, pat + ".log"))):
         lines = [l for l in open(f) if l.startswith("{")]
         if lines:
             d = json.loads(lines[-1])
             cfg = d["config"]
+            feats = (d.get("roofline") or {}).get("kernel_features") or []
             # passes per launch as the bench measured it (the fused kernel splits a step into
             # launches of at most 64 passes), as bench.py matches it
             nl = (d.get("roofline") or {}).get("launches")
@@ -49,6 +52,7 @@ if len(sys.argv) > 4:
            "fetch_reported_kib": g('FETCH_SIZE'), "write_reported_kib": g('WRITE_SIZE'),
            "scene": cfg.get("scene"), "width": cfg.get("width"), "height": cfg.get("height"),
            "passes_per_launch": ppl, "pass_streams": cfg.get("pass_streams"), "specialized": cfg.get("specialized", False),
+           "kernel": bench.kernel_kind(feats, cfg.get("pass_streams")),
            "source": "rocprofv3 --pmc SQ_INSTS_VALU / SQ_THREAD_CYCLES_VALU / SQ_ACTIVE_INST_VALU / "
                      "GRBM_GUI_ACTIVE / TCC_HIT_sum / TCC_MISS_sum (separate passes), scripts/pmc_summary.py"}
     # issue-weighted VALU occupancy when the instruction-mix passes ran (scripts/valu_weighted.py)
@@ -62,5 +66,5 @@ if len(sys.argv) > 4:
     data = json.load(open(out)) if os.path.exists(out) else {}
     if "scene" in data:                                   # an older single-record file
         data = {data.get("workload", "cornell1080"): data}
-    data[f'{rec["workload"]}@S{rec["pass_streams"]}'] = rec      # one record per workload and stream count
+    data[bench.pmc_key(rec["workload"], rec["kernel"], rec["pass_streams"])] = rec      # one record per workload and stream count
     json.dump(data, open(out, "w"), indent=1)

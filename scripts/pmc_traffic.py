@@ -9,6 +9,9 @@ by line_bytes / FETCH(gather20): HBM bytes at 128-B line granularity, an upper e
 counters include Infinity-Cache hits; the 30.7 MB table lives there)."""
 import csv, glob, json, os, sys
 
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402  (record keys: bench.kernel_kind / bench.pmc_key)
+
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
 out = sys.argv[2] if len(sys.argv) > 2 else "profiles/pmc_traffic.json"
 pat = sys.argv[3] if len(sys.argv) > 3 else "pmc*"          # the PMC runs of one workload
@@ -65,6 +68,7 @@ for f in sorted(glob.glob(os.path.join(root, pat + ".log"))):
         break
 rec = {"workload": cfg.get("workload", "cornell1080").split(":")[0], "scene": cfg.get("scene", "cornell"), "width": cfg.get("width", 1921), "height": cfg.get("height", 1081),
        "passes_per_launch": float(ppl), "pass_streams": cfg.get("pass_streams"), "specialized": cfg.get("specialized", False),
+       "kernel": bench.kernel_kind(roof.get("kernel_features") or [], cfg.get("pass_streams")),
        "fetch_reported_bytes_per_launch": int(fetch), "write_reported_bytes_per_launch": int(write),
        "fetch_scale": fscale, "write_scale": wscale,
        "hbm_bytes_per_launch": int(fetch * (fscale or 1.0) + write * (wscale or 1.0)),
@@ -72,11 +76,11 @@ rec = {"workload": cfg.get("workload", "cornell1080").split(":")[0], "scene": cf
        "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), x1024, calibrated",
        "method": __doc__}
 os.makedirs(os.path.dirname(out), exist_ok=True)
-# one record per workload and pass-stream count: {workload@S<streams>: record}
+# one record per workload and kernel: {bench.pmc_key: record}
 data = json.load(open(out)) if os.path.exists(out) else {}
 if "scene" in data:                                       # an older single-record file
     data = {data.get("workload", "cornell1080"): data}
-data[f'{rec["workload"]}@S{rec["pass_streams"]}'] = rec      # one record per workload and stream count
+data[bench.pmc_key(rec["workload"], rec["kernel"], rec["pass_streams"])] = rec      # one record per workload and stream count
 json.dump(data, open(out, "w"), indent=1)
 print(json.dumps({k: v for k, v in rec.items() if k not in ("method", "calibration")}))
 print(json.dumps(calib))

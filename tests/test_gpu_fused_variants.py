@@ -1,6 +1,6 @@
-"""The fused S = 1 kernel's round-3 variants against the oracle, bit for bit: grouped path
-regeneration (BDPT_REGEN_K, default 48 lanes), park-time prefetch (BDPT_PARK_PREFETCH) and paired
-segment loads (BDPT_RNG_PAIR, which the auto stream mode switches off where it measures slower).
+"""The fused S = 1 kernel's variants against the oracle, bit for bit: grouped path regeneration
+(BDPT_REGEN_K, default 48 lanes; 1 = restart at once, 64 = whole-wave lockstep) and paired segment
+loads (BDPT_RNG_PAIR, which the auto stream mode switches off where it measures slower).
 Each variant is a scene-specialised build selected through BDPT_JIT_FLAGS (its own JIT cache
 entry); the pass order of every pixel, and so its running mean, must be unchanged."""
 import os
@@ -14,7 +14,7 @@ from conftest import SCENES
 
 pytestmark = pytest.mark.gpu
 
-VARIANTS = ["", "-DBDPT_RNG_PAIR=0", "-DBDPT_PARK_PREFETCH=0", "-DBDPT_REGEN_K=1", "-DBDPT_REGEN_K=64"]
+VARIANTS = ["", "-DBDPT_RNG_PAIR=0", "-DBDPT_REGEN_K=1", "-DBDPT_REGEN_K=64"]
 
 
 @pytest.fixture(scope="module")

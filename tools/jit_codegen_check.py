@@ -35,21 +35,13 @@ def hexf(v):
 def jit_defines(spheres):
     """The -D options jit_path_kernel passes (same geometry literals: {p, rad*rad} in fp32)."""
     import numpy as np
-    parts, lrec, emis = [], [], 0
+    parts, emis = [], 0
     for i, s in enumerate(spheres):
         rr = np.float32(s["rad"]) * np.float32(s["rad"])
         parts.append("{" + ",".join(hexf(x) for x in (s["p"][0], s["p"][1], s["p"][2], rr)) + "}")
         if any(float(e) != 0.0 for e in s["e"]):
             emis |= 1 << i
-            r = np.float32(s["rad"])
-            area = np.float32(np.float32(np.float32(4.0) * np.float32(np.pi)) * r) * r
-            lrec.append("{" + ",".join(hexf(x) for x in (s["p"][0], s["p"][1], s["p"][2], r)) + "}")
-            lrec.append("{" + ",".join(hexf(x) for x in (s["e"][0], s["e"][1], s["e"][2], area)) + "}")
-    nl = len(lrec) // 2
-    if not lrec:
-        lrec = ["{0,0,0,0}", "{0,0,0,0}"]
     return [f"-DBDPT_JIT_N={len(spheres)}", f"-DBDPT_JIT_EMIS={emis}ull", "-DBDPT_JIT_GEOM={" + ",".join(parts) + "}",
-            f"-DBDPT_JIT_NL={nl}", "-DBDPT_JIT_LREC={" + ",".join(lrec) + "}",
             f"-DBDPT_JIT_ZERO_SAFE={int(zero_exit_safe(spheres))}"]
 
 
