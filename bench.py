@@ -632,8 +632,8 @@ def main():
             if "unit_fold" in features:
                 # ordered in-kernel fold: colors + counter read and written once per unit of
                 # kUnitPasses (8) passes, pixels once per launch; no radiance buffer
-                units = max(1.0, passes_per_launch / 8)
-                bytes_per_launch = own_pixels * (32 * units + 4) + samples_per_launch * 4 * w["rng_reads"]
+                per_unit = max(1.0, passes_per_launch / 8)          # units of a tile per launch
+                bytes_per_launch = own_pixels * (32 * per_unit + 4) + samples_per_launch * 4 * w["rng_reads"]
             elif r.last_streams > 1:
                 # pass streams: the path kernel reads the counter once and writes 12 B of radiance
                 # per sample; the fold kernel (not this launch) does the colors/pixels RMW
