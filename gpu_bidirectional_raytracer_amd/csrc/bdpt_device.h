@@ -99,16 +99,17 @@ struct bdpt_path_args {
     float bvh_c[3], bvh_r;          // ball around every BVH sphere (per-ray margin)
     float bvh_q;                    // 64u / smallest BVH radius (per-ray margin)
     unsigned long long* prof;       // BDPT_PROF builds: per-section shader cycles (8 counters)
-    // Ordered in-kernel fold (BDPT_UNITS builds of the pass-stream kernel): workgroup b renders
-    // unit (tile b % unit_wgs, range b / unit_wgs) = passes [range * unit_passes, ...) of its 32x8
-    // tile, one lane per pixel, with the running mean in registers; the units of a tile run in
-    // range order (a wave waits for its 8x8 tile's flag to reach epoch << 8 | range).
+    // Ordered in-kernel fold (BDPT_UNITS builds of the pass-stream kernel): a workgroup claims a
+    // unit (tile, range) = passes [range * unit_passes, ...) of a 32x8 tile, one lane per pixel,
+    // with the running mean in registers; the units of a tile run in range order (a wave waits for
+    // its 8x8 tile's flag to reach epoch << 8 | range).
     int unit_passes;                // passes per range
     int unit_wgs;                   // tile workgroups of the launch (gx * gy)
     int gx, gy;                     // the tile grid the 1-D unit grid enumerates
     unsigned unit_tag;              // this launch's epoch << 8
     unsigned* unit_flags;           // per 8x8 wave tile: epoch << 8 | ranges folded
     unsigned* unit_err;             // non-zero: a handover wait timed out (ordering violated)
+    unsigned* unit_ctr;             // per XCD queue: units claimed (8 counters, 128 B apart, zeroed per launch)
 };
 
 // Tile row of a workgroup row: identity, or the sub-th tile row of this shard's k-th band.

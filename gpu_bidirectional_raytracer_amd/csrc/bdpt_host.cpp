@@ -1341,14 +1341,15 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
             pool_ran = true;
         }
         if (unitsl) {
-            // 1-D grid of units in range-major order: workgroup b renders tile b % wgs, range b / wgs
+            // one workgroup per unit; each claims its unit from its XCD's queue (bdpt_kernels.hip)
             const int wgs = (int)grid.x * grid_rows;
             const int nranges = (a.npass + a.unit_passes - 1) / a.unit_passes;
             const size_t nflags = (size_t)wgs * 4;
-            if (!c->d_uerr) {
-                HIPCHK(c, hipMalloc(&c->d_uerr, sizeof(unsigned)));
+            if (!c->d_uerr) {                                // error word + 8 queue counters, 128 B apart
+                HIPCHK(c, hipMalloc(&c->d_uerr, sizeof(unsigned) * (32 + 8 * 32)));
                 HIPCHK(c, hipMemsetAsync(c->d_uerr, 0, sizeof(unsigned), c->stream));
             }
+            HIPCHK(c, hipMemsetAsync(c->d_uerr + 32, 0, sizeof(unsigned) * 8 * 32, c->stream));
             if (nflags > c->uflags_cap || ((c->uepoch + 1) & 0xffffffu) == 0) {
                 if (nflags > c->uflags_cap) {
                     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1364,6 +1365,7 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
             a.unit_tag = c->uepoch << 8;
             a.unit_flags = c->d_uflags;
             a.unit_err = c->d_uerr;
+            a.unit_ctr = c->d_uerr + 32;
             a.unit_wgs = wgs;
             a.gx = (int)grid.x;
             a.gy = grid_rows;
@@ -1420,7 +1422,7 @@ static int one_synchronize(bdpt_ctx* c) {
         HIPCHK(c, hipMemcpy(&e, c->d_uerr, sizeof e, hipMemcpyDeviceToHost));
         c->units_check = false;
         if (e) return fail(c, BDPT_EHIP, "path kernel: a unit waited too long for its tile's previous range "
-                                         "(in-order workgroup dispatch assumed; the frame is not valid)");
+                                         "(its predecessor did not finish within ~1 s; the frame is not valid)");
     }
     return fold_timing(c);
 }

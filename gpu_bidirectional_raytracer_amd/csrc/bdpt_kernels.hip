@@ -496,15 +496,15 @@ __device__ __forceinline__ float ld_coherent(float* p) {
 __device__ __forceinline__ void st_coherent(float* p, float v) {
     __hip_atomic_store((unsigned*)p, __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// Wait until *f == want.  The unit that sets it has a smaller workgroup id, so it was dispatched
-// earlier and is resident or done; the bound (~0.3 s) turns a broken assumption into an error
+// Wait until *f == want.  The unit that sets it was claimed earlier from the same queue, by a
+// workgroup that is running (or done); the bound (~1.3 s) turns a broken assumption into an error
 // report (*err) instead of a hang.
 __device__ __forceinline__ void unit_wait(unsigned* f, unsigned want, unsigned* err) {
     for (unsigned spins = 0;; spins++) {
         const unsigned v = __builtin_amdgcn_readfirstlane(
             __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
         if (v == want) break;
-        if (spins > (1u << 20)) {
+        if (spins > (1u << 22)) {
             __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             break;
         }
@@ -616,8 +616,35 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
     // order; a lane renders the range's passes of its pixel in order and keeps the running mean in
     // registers, and the units of a tile follow each other through per-wave-tile flags
     constexpr bool kUnits = STREAMS && BDPT_UNITS && !BDPT_POOL;
-    const unsigned urange = kUnits ? blockIdx.x / (unsigned)a.unit_wgs : 0u;
-    const int vtile = kUnits ? (int)(blockIdx.x - urange * (unsigned)a.unit_wgs) : 0;
+    // A workgroup claims its unit from the queue of its XCD (tiles t = xcd mod 8, range-major), or
+    // steals from the next queues; so a unit's predecessor (same tile, previous range, same queue)
+    // was claimed earlier by a running workgroup, whatever order the hardware dispatches in.  The
+    // grid has exactly one workgroup per unit.
+    unsigned urange = 0u;
+    int vtile = 0;
+    if constexpr (kUnits) {
+        __shared__ unsigned uclaim[2];
+        if (threadIdx.x == 0) {
+            const unsigned wgs = (unsigned)a.unit_wgs, nr = (unsigned)((a.npass + a.unit_passes - 1) / a.unit_passes);
+            const unsigned xcd = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 7u;   // XCC_ID
+            uclaim[0] = 0xffffffffu;
+            for (unsigned k = 0; k < 8u; k++) {
+                const unsigned q = (xcd + k) & 7u;
+                const unsigned ntq = wgs > q ? (wgs - q + 7u) / 8u : 0u;      // tiles of queue q
+                if (ntq == 0u) continue;
+                const unsigned u = atomicAdd(a.unit_ctr + q * 32u, 1u);
+                if (u < ntq * nr) {
+                    uclaim[0] = u / ntq;                                       // range
+                    uclaim[1] = q + 8u * (u - (u / ntq) * ntq);                // tile
+                    break;
+                }
+            }
+        }
+        __syncthreads();
+        urange = uclaim[0];
+        vtile = (int)uclaim[1];
+        if (urange == 0xffffffffu) return;                                     // (cannot happen)
+    }
     // the workgroup's tile (vbx, vby) in the tile grid (vgx, vgy)
     const int vbx = kUnits ? vtile % a.gx : (int)blockIdx.x, vby = kUnits ? vtile / a.gx : (int)blockIdx.y;
     const int vgx = kUnits ? a.gx : (int)gridDim.x, vgy = kUnits ? a.gy : (int)gridDim.y;
@@ -831,9 +858,9 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
     // (units: the counter before the unit's slot k is cnt0 + k)
     const unsigned uflag = kUnits ? (unsigned)vtile * 4u + (unsigned)wave : 0u;   // this wave's 8x8 tile
     if constexpr (kUnits) {
-        // the previous range of this tile has folded its passes (in-order WG dispatch makes that a
-        // short or no wait); colours and counter are read at the coherence point (agent-scope
-        // relaxed atomics: the previous unit may have run on another XCD, whose L2 is not ours)
+        // the previous range of this tile has folded its passes (it was claimed a queue's worth of
+        // units earlier: a short wait or none); colours and counter are read at the coherence point
+        // (agent-scope relaxed atomics: a stolen unit may have run on another XCD, whose L2 is not ours)
         if (urange > 0) unit_wait(a.unit_flags + uflag, a.unit_tag | urange, a.unit_err);
         if (active) {
             col.x = ld_coherent(&a.colors[i].x);
