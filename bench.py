@@ -670,7 +670,7 @@ def main():
                                      f"some of it ({', '.join(skips)}: results unchanged), so frac measures "
                                      "work delivered, not VALU efficiency -- see valu_busy_pmc (2 cycles per VALU instruction) and "
                                      "valu_issue_occupancy_pmc (the instruction mix priced at measured gfx950 issue costs, "
-                                     "DESIGN.md section 10)")
+                                     "DESIGN.md section 4, Roofline)")
             vrec = _pmc_record("pmc_valu.json", args.workload, wl["scene"], W, H, passes_per_launch,
                                r.last_streams, r.last_specialized, kind) if single else None
             if vrec:
