@@ -45,6 +45,7 @@ extern "C" __global__ void bdpt_light_kernel(const bdpt_dev_sphere*, unsigned, c
 extern "C" const void* bdpt_path_kernel_table[36];   // [(S > 1) * 18 + (BVH ? 17 : n <= 16 ? n : 0)]
 extern "C" __global__ void bdpt_pixels_kernel(const bdpt_dev_vec*, uchar4*, const float*, int);
 extern "C" __global__ void bdpt_accum_kernel(bdpt_path_args);
+extern "C" __global__ void bdpt_accum_serial_kernel(bdpt_path_args);
 
 extern "C" __global__ void bdpt_frame_add_kernel(float*, const float*, unsigned*, const unsigned*, int);
 
@@ -849,8 +850,13 @@ void bdpt_destroy(bdpt_ctx* c) {
     if (c->fstream) (void)hipStreamSynchronize(c->fstream);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->d_prof) {                 // section profile of a -DBDPT_PROF kernel (experiments)
-        unsigned long long p[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (hipMemcpy(p, c->d_prof, sizeof p, hipMemcpyDeviceToHost) == hipSuccess) {
+        unsigned long long p[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+        const char* pe = getenv("BDPT_PROF");
+        if (pe && !strcmp(pe, "counts") && hipMemcpy(p, c->d_prof, sizeof p, hipMemcpyDeviceToHost) == hipSuccess) {
+            fprintf(stderr, "bdpt_counts");        // region counts of a -DBDPT_COUNTS kernel
+            for (int q = 0; q < 16; q++) fprintf(stderr, " %llu", p[q]);
+            fprintf(stderr, "\n");
+        } else if (hipMemcpy(p, c->d_prof, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost) == hipSuccess) {
             double tot = 0;
             for (int q = 0; q < 6; q++) tot += (double)p[q];
             fprintf(stderr, "bdpt_prof waves=%llu cycles/wave=%.0f", p[7], p[7] ? tot / p[7] : 0.0);
@@ -1088,8 +1094,8 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
     a.orig[0] = cam.orig.x; a.orig[1] = cam.orig.y; a.orig[2] = cam.orig.z;
     a.shard = c->shard; a.nshards = c->nshards; a.band_rows = c->band_rows;
     if (!c->d_prof && getenv("BDPT_PROF")) {
-        HIPCHK(c, hipMalloc(&c->d_prof, 8 * sizeof(unsigned long long)));
-        HIPCHK(c, hipMemset(c->d_prof, 0, 8 * sizeof(unsigned long long)));
+        HIPCHK(c, hipMalloc(&c->d_prof, 16 * sizeof(unsigned long long)));
+        HIPCHK(c, hipMemset(c->d_prof, 0, 16 * sizeof(unsigned long long)));
     }
     a.prof = c->d_prof;
 
@@ -1380,7 +1386,11 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
         else
             HIPCHK(c, hipLaunchKernel(kern, grid, block, kargs, smem, c->stream));
         HIPCHK(c, hipEventRecord(cs.kev[2 * launches + 1], c->stream));
-        if (st && !unitsl) {                                // the ordered fold, on fstream
+        static const bool fold_serial = getenv("BDPT_FOLD_SERIAL") != nullptr;   // experiment
+        if (st && !unitsl && fold_serial) {                 // the fold after the path kernel
+            grid.z = 1;
+            HIPCHK(c, hipLaunchKernel((const void*)&bdpt_accum_serial_kernel, grid, block, kargs, 0, c->stream));
+        } else if (st && !unitsl) {                         // the ordered fold, on fstream
             grid.z = 1;
             HIPCHK(c, hipEventRecord(c->rb_path_ev[half], c->stream));
             HIPCHK(c, hipStreamWaitEvent(c->fstream, c->rb_path_ev[half], 0));

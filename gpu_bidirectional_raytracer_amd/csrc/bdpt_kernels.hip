@@ -763,6 +763,16 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
 #else
 #define BDPT_TICK(k) do { } while (0)
 #endif
+#ifdef BDPT_COUNTS
+    // region counts (experiments; DESIGN_LOG "instruction attribution"): how often the wave
+    // executes each region (the region's condition holds for some lane), added to a.prof[0..15]
+    unsigned long long pcnt[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#define BDPT_CNT(k, cond) do { if (__builtin_amdgcn_ballot_w64(cond) != 0) pcnt[k]++; } while (0)
+#define BDPT_CNTN(k, n) do { pcnt[k] += (n); } while (0)
+#else
+#define BDPT_CNT(k, cond) do { } while (0)
+#define BDPT_CNTN(k, n) do { } while (0)
+#endif
     int x = vbx * BDPT_BTW + (wave % BDPT_BLOCK_WX) * BDPT_WTW + (lane % BDPT_WTW);
     int ly = vby * BDPT_BTH + (wave / BDPT_BLOCK_WX) * BDPT_WTH + (lane / BDPT_WTW);
     // Frame edges packed into full waves (rows not remapped to shard bands): a frame whose width
@@ -924,7 +934,11 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
     bool alive = active && nslot > 0 && cnt0 + (unsigned)(kUnits ? k : s0 + k * S) < BDPT_DEV_COUNTER_CAP;
 
     // (a pool lane without a pixel yet keeps the loop going: it draws one at the iteration's end)
+    BDPT_CNTN(14, 1);
     while (__builtin_amdgcn_ballot_w64(alive || (kPool && want)) != 0) {   // wave-uniform loop
+        BDPT_CNTN(0, 1);
+        BDPT_CNT(1, alive && fresh);
+        BDPT_CNT(2, alive);
 #ifdef BDPT_STATS
         {
             const unsigned long long ma = __builtin_amdgcn_ballot_w64(alive);
@@ -999,8 +1013,10 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                     unsigned kt = key_of(t);
                     auto hit = [&](int s) -> bool {
                         const tdet qd = sphere_det(geom(s), ro, rd);
-                        if (small_sphere(s) && __builtin_amdgcn_ballot_w64(!(qd.det < 0.f)) == 0)
+                        if (small_sphere(s) && __builtin_amdgcn_ballot_w64(!(qd.det < 0.f)) == 0) {
+                            BDPT_CNTN(10, 1);
                             return true;                          // every lane misses sphere s
+                        }
                         const troots q = roots_of(qd);
                         const unsigned nk = umin3(kt, key_of(q.t1), key_of(q.t2));
                         id = nk < kt ? s : id;
@@ -1023,6 +1039,7 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
             done = id < 0;
         }
         BDPT_TICK(0);                 // camera ray + closest hit
+        BDPT_CNT(3, alive && !done);
         // paired loads: an odd-depth segment takes the randoms loaded with the previous one --
         // here, after the closest hit and just before the shading uses them, not where the next
         // loads are issued: a copy there made the compiler merge the loaded values through
@@ -1065,6 +1082,7 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                     // per lane, so the results are unchanged.
                     const bool isdiff = (mat & 255) == BDPT_DEV_DIFF;
                     const f3 cc = mk(cm.x, cm.y, cm.z);
+                    BDPT_CNT(4, true);
                     // the path's last segment (depth 6, :621): the next direction and the
                     // specular weights are never used -- a diffuse vertex still weights its NEE
                     if (depth >= 6u) {
@@ -1095,6 +1113,7 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                             } else {
                                 refr = true;
                             }
+                            BDPT_CNT(5, refr);
                         }
                     }
                     if (isdiff || refr) {
@@ -1147,6 +1166,7 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
             auto lrec = [&](int k) -> float4 { return ld_const(a.lightrec, k); };
             const int nsteps = nlights > 0 ? nlights : 1;
             for (int li = 0; li < nsteps; li++) {                         // uniform
+                BDPT_CNTN(6, 1);
                 bool has_nee = false, has_vlp = false;
                 f3 sd = res, con = res;
                 float maxt = 0.f, vmaxt = 0.f;
@@ -1238,6 +1258,7 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                         int lg = c <= 8 ? 3 : (c <= 16 ? 2 : (c <= 32 ? 1 : 0));
                         while (lg > 0 && (1 << lg) > n) lg--;
                         if (lg > 0) {
+                            BDPT_CNTN(8, 1);
                             const int rpg = 64 >> lg;
                             const int r = lane & (rpg - 1), g = lane >> (6 - lg);
                             unsigned occ = 0;
@@ -1303,7 +1324,9 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
 #if BDPT_IKEY
                         const unsigned km = maxt_key(r0.w);
 #endif
+                        BDPT_CNTN(7, 1);
                         auto step = [&](int s) -> bool {                  // IntersectP(Vacuum)Device
+                            BDPT_CNTN(9, 1);
                             const tdet qd = sphere_det(geom(s), o, d);
                             if (small_sphere(s) && __builtin_amdgcn_ballot_w64(!(qd.det < 0.f)) == 0)
                                 return true;                          // every ray misses sphere s
@@ -1356,6 +1379,8 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
         if constexpr (STREAMS) asm volatile("" ::"v"(q0), "v"(q1), "v"(q2), "v"(q3), "v"(q4));
         if (alive) {
             if (!done && ++depth > 6) done = true;                       // :621 7-segment cap
+            BDPT_CNT(11, done);
+            BDPT_CNTN(15, __popcll(__builtin_amdgcn_ballot_w64(done)));
             if (done) {                                                  // :774-787
                 if constexpr (!STREAMS || kUnits) {
                     const unsigned cnt = cnt0 + (unsigned)k;      // S == 1: pass k
@@ -1454,6 +1479,7 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
             // release the parked lanes together (wave-uniform decision)
             const unsigned long long mp = __builtin_amdgcn_ballot_w64(parked);
             if (mp != 0 && (__popcll(mp) >= BDPT_REGEN_K || __builtin_amdgcn_ballot_w64(alive) == 0)) {
+                BDPT_CNTN(13, 1);
                 if (parked) {
                     parked = false;
                     alive = true;
@@ -1477,6 +1503,10 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
         for (int q = 0; q < 6; q++) atomicAdd(&a.prof[q], pacc[q]);
         atomicAdd(&a.prof[7], 1ull);
     }
+#endif
+#ifdef BDPT_COUNTS
+    if (lane == 0 && a.prof)
+        for (int q = 0; q < 16; q++) atomicAdd(&a.prof[q], pcnt[q]);
 #endif
     if constexpr (kUnits) {
         // the unit's result, then this wave tile's flag: the next range's unit may start
@@ -1518,7 +1548,8 @@ extern "C" const void* bdpt_path_kernel_table[36] = {BDPT_ROW(false), BDPT_ROW(t
 // Ordered fold of pass-stream radiance (S > 1): the running mean of device.cu:774-787 applied
 // to rbuf[0..npass) in pass order, so the result is the S == 1 result bit for bit.  Same grid
 // rows (and shard remap) as the path launch; one thread per pixel.
-extern "C" __global__ __launch_bounds__(256) void bdpt_accum_kernel(bdpt_path_args a) {
+template <int U>
+__device__ __forceinline__ void accum_body(const bdpt_path_args& a) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #ifdef BDPT_PROF
     // section profile (experiments): shader cycles per wave between wave-uniform points, summed
@@ -1557,12 +1588,24 @@ extern "C" __global__ __launch_bounds__(256) void bdpt_accum_kernel(bdpt_path_ar
     };
     // (folds with 8 loads in flight, or with streaming loads, ran faster alone but slowed the
     // concurrent path kernel more: caustic8 -1.3 % (round 2), -4 to -13 % (profiles/r05_s3_*))
-    for (int p = 0; p < n; p++) fold(rb[(size_t)p * a.nloc]);
+    int p = 0;
+    if constexpr (U > 1) {                   // U loads in flight (the fold after the path kernel)
+        for (; p + U <= n; p += U) {
+            bdpt_dev_vec v[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) v[u] = rb[(size_t)(p + u) * a.nloc];
+#pragma unroll
+            for (int u = 0; u < U; u++) fold(v[u]);
+        }
+    }
+    for (; p < n; p++) fold(rb[(size_t)p * a.nloc]);
     if (cnt == cnt0) return;
     a.colors[i] = col;
     a.counter[i] = cnt;
     a.pixels[i] = bdpt_dev_to_rgba(col.x, col.y, col.z, a.gamma_thr);
 }
+extern "C" __global__ __launch_bounds__(256) void bdpt_accum_kernel(bdpt_path_args a) { accum_body<1>(a); }
+extern "C" __global__ __launch_bounds__(256) void bdpt_accum_serial_kernel(bdpt_path_args a) { accum_body<16>(a); }
 
 // Frame assembly of a multi-device context without RCCL: add a peer's zero-padded frame (exact:
 // each pixel is non-zero on one device only, and x + 0 == x).
