@@ -1328,8 +1328,10 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                         auto step = [&](int s) -> bool {                  // IntersectP(Vacuum)Device
                             BDPT_CNTN(9, 1);
                             const tdet qd = sphere_det(geom(s), o, d);
-                            if (small_sphere(s) && __builtin_amdgcn_ballot_w64(!(qd.det < 0.f)) == 0)
+                            if (small_sphere(s) && __builtin_amdgcn_ballot_w64(!(qd.det < 0.f)) == 0) {
+                                BDPT_CNTN(12, 1);
                                 return true;                          // every ray misses sphere s
+                            }
                             const troots q = roots_of(qd);
 #if BDPT_IKEY
                             unsigned long long h = __builtin_amdgcn_ballot_w64(

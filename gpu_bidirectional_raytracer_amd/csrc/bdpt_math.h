@@ -91,15 +91,9 @@ BDPT_HD void bdpt_sincos_tab(double x, const double* sintab, double* so, double*
 #ifndef BDPT_SQRT_SHIFT
 #define BDPT_SQRT_SHIFT 1
 #endif
-#ifndef BDPT_SQRT_ONESIDED
-#define BDPT_SQRT_ONESIDED 0
-#endif
 #if defined(__HIPCC__)
 // v_sqrt_f32 + the +-1 ulp residual correction: correctly rounded for x >= 2^-96 and x == 0.
 __device__ __forceinline__ float bdpt_sqrt_rn_core(float x) {
-#ifdef BDPT_ABL_SQRT
-    return __builtin_amdgcn_sqrtf(x);
-#endif
 #if BDPT_SQRT_SHIFT
     // The same decision without VCC selects (+5 % on the path kernel with the det test dropped,
     // bdpt_kernels.hip sphere_isect_inf): the residuals are taken with the opposite sign,
@@ -122,16 +116,10 @@ __device__ __forceinline__ float bdpt_sqrt_rn_core(float x) {
     const float sup = __int_as_float(__float_as_int(s) + 1);
     const float rdn = __builtin_fmaf(-sdn, s, x);
     const float rup = __builtin_fmaf(-sup, s, x);
-#if BDPT_SQRT_ONESIDED == 1
-    (void)rdn;
-    s = rup > 0.f ? sup : s;
-#elif BDPT_SQRT_ONESIDED == 2
-    (void)rup;
-    s = rdn <= 0.f ? sdn : s;
-#else
+    // the select form (BDPT_SQRT_SHIFT=0: the reference decision scripts/sqrt_shift_check.hip
+    // compares the sign-bit form with)
     s = rdn <= 0.f ? sdn : s;
     s = rup > 0.f ? sup : s;
-#endif
     return s;
 }
 

@@ -143,3 +143,18 @@ def test_zero_exit_rule():
         else:
             sp[k]["p"] = sp[k]["p"] + rng.normal(0, 20, 3)
         assert jc.zero_exit_safe(sp) == _c_rule(sp), (t, sp[k])
+
+
+def test_valu_attribution_anchors():
+    """tools/valu_attrib.py finds its section anchors in the kernel source, in order, and every
+    counter slot it reads has a BDPT_CNT / BDPT_CNTN site (the instrumentation is compiled only
+    with -DBDPT_COUNTS, so the production build is untouched)."""
+    import re
+    import valu_attrib as va
+    secs, (k0, kend) = va.sections()
+    assert k0 < secs[1][1] and secs[-1][2] <= kend
+    for (_, a, b), (_, c, _) in zip(secs, secs[1:]):
+        assert a <= b and (c > b or c < a), secs         # ranges do not overlap
+    src = open(va.SRC).read()
+    sites = {int(m.group(1)) for m in re.finditer(r"BDPT_CNTN?\((\d+),", src)}
+    assert sites >= set(range(16)) - {va.C_REFR}, sorted(sites)
