@@ -96,6 +96,12 @@ def static_counts(scene, units, keep=None):
     blocks = out.strip().split("\n\n")
     assert len(blocks) == len(insts), (len(blocks), len(insts))
 
+    # the exec-masked fallbacks for out-of-range operands (library sqrt / division; the wave
+    # branches over them when no lane needs them): priced apart, not in the estimate
+    src = open(SRC).read().split("\n")
+    cold = {i + 1 for i, l in enumerate(src)
+            if re.search(r"return 1\.f / x;|\*root = sqrtf\(x\);|return 1\.f / \*root;|kq = na / nb;", l)}
+
     def section(ln):
         for name, a, b in secs:
             if a <= ln <= b:
@@ -106,6 +112,10 @@ def static_counts(scene, units, keep=None):
         fr = blk.split("\n")
         frames = [(fr[i], fr[i + 1]) for i in range(0, len(fr) - 1, 2)]
         sec, part = "other", ""
+        if any(int(m.group(1)) in cold for _, loc in frames
+               for m in [re.search(r"bdpt_kernels\.hip:(\d+)", loc)] if m):
+            cnt[("cold", "valu" if op.startswith("v_") else "other")] += 1
+            continue
         for fn, loc in frames:
             m = re.search(r"bdpt_kernels\.hip:(\d+)", loc)
             if m and k0 <= int(m.group(1)) <= kend:
@@ -161,7 +171,10 @@ def attribute(cnt, c, n_spheres, n_small):
         "path end / accumulation / RNG loads": v("path_end") * c[C_ITER],
         "regen release": v("regen_release") * c[C_REGEN],
     }
-    return {k: x / paths for k, x in rows.items()}, {
+    # per path in the PMC's sense: wave instructions per 64 paths (a wave instruction serves 64
+    # lanes; scripts/pmc_summary.py valu_insts_per_wave = SQ_INSTS_VALU / SQ_WAVES, over the
+    # paths per lane of the launch)
+    return {k: x * 64 / paths for k, x in rows.items()}, {
         "waves": waves, "paths": paths, "iterations_per_wave": c[C_ITER] / waves,
         "segments_per_path": c[C_HIT] * 64 / paths if paths else None,
         "closest_hit_small_skips": c[C_CHSKIP] / max(1, n_small * c[C_HIT]),
@@ -177,7 +190,7 @@ def main():
     ap.add_argument("scene", nargs="?", default=os.path.join(REPO, "assets", "scenes", "cornell.scn"))
     ap.add_argument("--units", action="store_true", help="the in-kernel fold build (-DBDPT_UNITS=1)")
     ap.add_argument("--counts", help="file holding a bdpt_counts line")
-    ap.add_argument("--pmc-valu", type=float, help="measured SQ_INSTS_VALU per path")
+    ap.add_argument("--pmc-valu", type=float, help="measured SQ_INSTS_VALU per wave and path per lane")
     ap.add_argument("--keep")
     args = ap.parse_args()
     cnt = static_counts(args.scene, args.units, args.keep)
