@@ -77,6 +77,7 @@ struct bdpt_ctx {
         std::vector<hipEvent_t> kev;               // per path-kernel launch {before, after}
         int launches = 0;
         bool pending = false;                      // issued, not folded yet
+        bool serial_fold = false;                  // its folds ran after its path kernels, in-stream
     } ring[kRing];
     long long issued = 0, folded = 0;   // calls issued / folded into the accumulators
     double acc_ms = 0.0;         // accumulated device time of finished path-pass calls
@@ -733,8 +734,9 @@ static int fold_timing(bdpt_ctx* c, long long upto) {
         // kernels and costs about that much of its own time in back-to-back calls: caustic pools
         // 3.79 ms kernels + 1.10 ms fold -> 4.05 ms per call, two passes per lane 4.85 + 0.84 ->
         // 4.95, profiles/r04_s20_*)
+        // (a call whose folds ran on its own stream after its path kernels is charged in full)
         for (int r = 0; r < bdpt_ctx::kTunePhases; r++)
-            if (c->folded == c->tune_call[r]) c->tune_ms[r] = kms + 0.25 * ((double)ms - kms);
+            if (c->folded == c->tune_call[r]) c->tune_ms[r] = s.serial_fold ? (double)ms : kms + 0.25 * ((double)ms - kms);
         c->acc_launches += s.launches;
         s.pending = false;
     }
@@ -1264,9 +1266,17 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
         if (st && !jf_pool && !jf_units && !jf_streams) jf_streams = jit_path_kernel(c, true);
         if (!st && !jf_fused) jf_fused = jit_path_kernel(c, false, pair);
     }
-    // a fused launch updates colors itself: it waits for the outstanding fold, before the call's
-    // timing starts (so the stream-mode measurement does not charge that fold to it)
-    if (any_fused || jf_units)
+    // Pixel pools fold on the context's stream right after each path kernel (serial fold): the
+    // concurrent fold's HBM traffic slowed the next call's pooled path kernel more than the fold
+    // costs on its own -- caustic pools 4.10 -> 4.04-4.07 ms per call, path kernel 3.93 -> 3.29-3.31
+    // ms; two passes per lane keep the concurrent fold (cornell S = 64 33.82 -> 33.92 ms serial),
+    // profiles/r05_s11_serial_fold.txt.  BDPT_FOLD_SERIAL=0/1 forces either (experiments).
+    static const int fold_env = getenv("BDPT_FOLD_SERIAL") ? atoi(getenv("BDPT_FOLD_SERIAL")) : -1;
+    const bool serial_fold = fold_env >= 0 ? fold_env > 0 : jf_pool != nullptr;
+    // a fused launch updates colors itself, and a serial fold does so on this stream: they wait
+    // for the outstanding concurrent fold, before the call's timing starts (so the stream-mode
+    // measurement does not charge that fold to it)
+    if (any_fused || jf_units || serial_fold)
         if (int rc = join_fold(c)) return rc;
     HIPCHK(c, hipEventRecord(cs.ev0, c->stream));
     int launches = 0;
@@ -1386,8 +1396,7 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
         else
             HIPCHK(c, hipLaunchKernel(kern, grid, block, kargs, smem, c->stream));
         HIPCHK(c, hipEventRecord(cs.kev[2 * launches + 1], c->stream));
-        static const bool fold_serial = getenv("BDPT_FOLD_SERIAL") != nullptr;   // experiment
-        if (st && !unitsl && fold_serial) {                 // the fold after the path kernel
+        if (st && !unitsl && serial_fold) {                 // the fold after the path kernel
             grid.z = 1;
             HIPCHK(c, hipLaunchKernel((const void*)&bdpt_accum_serial_kernel, grid, block, kargs, 0, c->stream));
         } else if (st && !unitsl) {                         // the ordered fold, on fstream
@@ -1407,6 +1416,7 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
     HIPCHK(c, hipEventRecord(cs.ev1, c->fold_pending ? c->fstream : c->stream));
     cs.launches = launches;
     cs.pending = true;
+    cs.serial_fold = serial_fold;
     if (tune_role >= 0) {
         c->tune_real[tune_role] = tune_role == 2 || tune_role == 5 ? quarter_ran
                                   : tune_role == 1 || tune_role == 4 ? (jf_fused != nullptr || tune_role == 1)
