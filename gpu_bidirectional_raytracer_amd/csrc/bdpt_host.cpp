@@ -852,11 +852,11 @@ void bdpt_destroy(bdpt_ctx* c) {
     if (c->fstream) (void)hipStreamSynchronize(c->fstream);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->d_prof) {                 // section profile of a -DBDPT_PROF kernel (experiments)
-        unsigned long long p[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+        unsigned long long p[24] = {};
         const char* pe = getenv("BDPT_PROF");
         if (pe && !strcmp(pe, "counts") && hipMemcpy(p, c->d_prof, sizeof p, hipMemcpyDeviceToHost) == hipSuccess) {
             fprintf(stderr, "bdpt_counts");        // region counts of a -DBDPT_COUNTS kernel
-            for (int q = 0; q < 16; q++) fprintf(stderr, " %llu", p[q]);
+            for (int q = 0; q < 24; q++) fprintf(stderr, " %llu", p[q]);
             fprintf(stderr, "\n");
         } else if (hipMemcpy(p, c->d_prof, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost) == hipSuccess) {
             double tot = 0;
@@ -1096,8 +1096,8 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
     a.orig[0] = cam.orig.x; a.orig[1] = cam.orig.y; a.orig[2] = cam.orig.z;
     a.shard = c->shard; a.nshards = c->nshards; a.band_rows = c->band_rows;
     if (!c->d_prof && getenv("BDPT_PROF")) {
-        HIPCHK(c, hipMalloc(&c->d_prof, 16 * sizeof(unsigned long long)));
-        HIPCHK(c, hipMemset(c->d_prof, 0, 16 * sizeof(unsigned long long)));
+        HIPCHK(c, hipMalloc(&c->d_prof, 24 * sizeof(unsigned long long)));
+        HIPCHK(c, hipMemset(c->d_prof, 0, 24 * sizeof(unsigned long long)));
     }
     a.prof = c->d_prof;
 

@@ -764,11 +764,15 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
 #define BDPT_TICK(k) do { } while (0)
 #endif
 #ifdef BDPT_COUNTS
-    // region counts (experiments; DESIGN_LOG "instruction attribution"): how often the wave
-    // executes each region (the region's condition holds for some lane), added to a.prof[0..15]
-    unsigned long long pcnt[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-#define BDPT_CNT(k, cond) do { if (__builtin_amdgcn_ballot_w64(cond) != 0) pcnt[k]++; } while (0)
-#define BDPT_CNTN(k, n) do { pcnt[k] += (n); } while (0)
+    // region counts (experiments; tools/valu_attrib.py): how often the wave executes each region
+    // (the region's condition holds for some lane).  The first active lane counts (inside
+    // divergent code a per-lane counter of a fixed lane would miss the events it sits out); the
+    // lanes' counts are summed at the end and added to a.prof[0..kCnt).
+    constexpr int kCnt = 24;
+    unsigned pcnt[kCnt] = {};
+    auto first_lane = [&]() { return lane == __builtin_ctzll(__builtin_amdgcn_ballot_w64(true)); };
+#define BDPT_CNT(k, cond) do { if (__builtin_amdgcn_ballot_w64(cond) != 0 && first_lane()) pcnt[k]++; } while (0)
+#define BDPT_CNTN(k, n) do { const unsigned n_ = (n); if (first_lane()) pcnt[k] += n_; } while (0)
 #else
 #define BDPT_CNT(k, cond) do { } while (0)
 #define BDPT_CNTN(k, n) do { } while (0)
@@ -1086,6 +1090,7 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                     // the path's last segment (depth 6, :621): the next direction and the
                     // specular weights are never used -- a diffuse vertex still weights its NEE
                     if (depth >= 6u) {
+                        BDPT_CNT(19, isdiff);
                         if (isdiff) {
                             specular = false;
                             thr = mul(thr, cc);
@@ -1096,6 +1101,8 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                     bool refr = false, into = false;
                     float nnt = 0.f, ddn = 0.f, cos2t = 0.f;
                     const float nc = 1.f, nt = 1.5f;
+                    BDPT_CNT(17, !isdiff);
+                    BDPT_CNT(18, isdiff);
                     if (!isdiff) {
                         specular = true;
                         refl = sub(rd, smul(2.f * dot(normal, rd), normal));
@@ -1203,6 +1210,7 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                     // a VLP with zero radiance adds exactly +0 to vres whether it is visible or
                     // not (wi * wo is finite): no ray.  Wave-uniform under pass streams, where a
                     // workgroup renders one pass (zero VLPs: cornell 6 %, cornell_glass 45 %)
+                    BDPT_CNT(20, !(v0.w == 0.f && v1.x == 0.f && v1.y == 0.f));
                     if (!(v0.w == 0.f && v1.x == 0.f && v1.y == 0.f)) {
                         vsd = sub(mk(v0.x, v0.y, v0.z), ro);
                         float len;
@@ -1270,6 +1278,7 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                                 const unsigned km = maxt_key(r0.w);
 #endif
                                 for (int s = n - 1 - g; s >= 0; s -= 1 << lg) {
+                                    BDPT_CNTN(16, 1);
                                     const troots q = sphere_roots(G[s], o, d);
 #if BDPT_IKEY
                                     if (umin2(key_of(q.t1), key_of(q.t2)) < km && !(vac && emissive(s))) { occ = 1; break; }
@@ -1507,8 +1516,15 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
     }
 #endif
 #ifdef BDPT_COUNTS
-    if (lane == 0 && a.prof)
-        for (int q = 0; q < 16; q++) atomicAdd(&a.prof[q], pcnt[q]);
+    if (a.prof) {
+        const unsigned long long live = __builtin_amdgcn_ballot_w64(true);
+        for (int q = 0; q < kCnt; q++) {
+            unsigned long long sum = 0;
+            for (unsigned long long m = live; m != 0; m &= m - 1)
+                sum += (unsigned)__builtin_amdgcn_readlane((int)pcnt[q], __builtin_ctzll(m));
+            if (lane == __builtin_ctzll(live) && sum != 0) atomicAdd(&a.prof[q], sum);
+        }
+    }
 #endif
     if constexpr (kUnits) {
         // the unit's result, then this wave tile's flag: the next range's unit may start

@@ -33,7 +33,9 @@ SRC = os.path.join(REPO, "gpu_bidirectional_raytracer_amd", "csrc", "bdpt_kernel
 LLVM = os.path.join(jcc.ROCM, "lib", "llvm", "bin")
 # counter slots (bdpt_kernels.hip BDPT_CNT / BDPT_CNTN sites)
 C_ITER, C_CAM, C_HIT, C_SHADE, C_BLOCK, C_REFR, C_LIGHT, C_FULL, C_SPLIT, C_STEP, C_CHSKIP, \
-    C_END, C_SHSKIP, C_REGEN, C_WAVES, C_PATHS = range(16)
+    C_END, C_SHSKIP, C_REGEN, C_WAVES, C_PATHS, C_SPLIT_IT, C_NONDIFF, C_DIFFDIR, C_LASTDIFF, \
+    C_VLP = range(21)
+NCOUNT = 24
 
 
 def sections():
@@ -51,9 +53,18 @@ def sections():
     ch = find(r"// closest hit, scanning", cam)
     t0 = find(r"BDPT_TICK\(0\)", ch)
     blk = find(r"const bool isdiff =", t0)
-    blk_end = find(r"ro = hit;", blk)
+    last = find(r"if \(depth >= 6u\) \{", blk)
+    nxt = find(r"f3 refl = rd;", last)
+    sr = find(r"if \(!isdiff\) \{", nxt)
+    dirb = find(r"if \(isdiff \|\| refr\) \{", sr)
+    fres = find(r"const float aa = nt - nc", dirb)
+    fres_end = find(r"rd = reflect \? refl : U;", fres)
+    blk_end = find(r"ro = hit;", fres_end)
     t1 = find(r"BDPT_TICK\(1\)", blk_end)
-    t2 = find(r"BDPT_TICK\(2\)", t1)
+    vlp = find(r"if \(diff && li == 0\) \{", t1)
+    vlp_in = find(r"BDPT_CNT\(20,", vlp)
+    vlp_end = find(r"// compact this step's shadow rays", vlp_in)
+    t2 = find(r"BDPT_TICK\(2\)", vlp_end)
     split = find(r"if \(lg > 0\) \{", t2)
     split_end = find(r"continue;", split)
     t3 = find(r"BDPT_TICK\(3\)", split_end)
@@ -62,8 +73,11 @@ def sections():
     t5 = find(r"BDPT_TICK\(5\)", regen)
     end = find(r"^}", t5)
     return [("prologue", k0, loop - 1), ("loop_control", loop, cam - 1), ("camera", cam, ch - 1),
-            ("closest_hit", ch, t0), ("shading", t0 + 1, blk - 1), ("diff_refr_block", blk, blk_end),
-            ("shading", blk_end + 1, t1), ("nee_vlp_setup", t1 + 1, t2), ("shadow_split", split, split_end),
+            ("closest_hit", ch, t0), ("shading", t0 + 1, blk - 1), ("block_head", blk, last - 1),
+            ("last_segment", last, nxt - 1), ("block_head", nxt, sr - 1), ("spec_refr_head", sr, dirb - 1),
+            ("fresnel", fres, fres_end), ("next_direction", dirb, blk_end),
+            ("shading", blk_end + 1, t1), ("nee_setup", t1 + 1, vlp_in), ("vlp_setup", vlp_in + 1, vlp_end - 1),
+            ("queue_push", vlp_end, t2), ("shadow_split", split, split_end),
             ("shadow_full", t2 + 1, t3), ("shadow_results", t3 + 1, t4), ("path_end", t4 + 1, regen - 1),
             ("regen_release", regen, t5), ("epilogue", t5 + 1, end)], (k0, end)
 
@@ -143,7 +157,8 @@ def parse_counts(path):
     for line in open(path):
         m = re.search(r"bdpt_counts\s+(.*)", line)
         if m:
-            return [int(x) for x in re.findall(r"\d+", m.group(1))][:16]
+            c = [int(x) for x in re.findall(r"\d+", m.group(1))][:NCOUNT]
+            return c + [0] * (NCOUNT - len(c))
     raise SystemExit(f"no bdpt_counts line in {path}")
 
 
@@ -161,9 +176,16 @@ def attribute(cnt, c, n_spheres, n_small):
         "closest hit: roots": ch_roots * (n_spheres * c[C_HIT] - c[C_CHSKIP]),
         "closest hit: rest": v("closest_hit") * c[C_HIT],
         "shading (hit point, normal, emitter)": v("shading") * c[C_SHADE],
-        "diffuse / specular / refraction block": v("diff_refr_block") * c[C_BLOCK],
-        "NEE / VLP set-up + queue push": v("nee_vlp_setup") * c[C_LIGHT],
-        "shadow split rounds": (v("shadow_split") + v("shadow_split:det") + v("shadow_split:roots")) * c[C_SPLIT],
+        "material decode (non-emitter block)": v("block_head") * c[C_BLOCK],
+        "last segment (depth 6)": v("last_segment") * c[C_LASTDIFF],
+        "specular / refraction set-up": v("spec_refr_head") * c[C_NONDIFF],
+        "next direction (cosine / transmitted)": v("next_direction") * c[C_DIFFDIR],
+        "Fresnel weights": v("fresnel") * c[C_REFR],
+        "NEE set-up (light sample, direction, weight)": v("nee_setup") * c[C_LIGHT],
+        "VLP set-up": v("vlp_setup") * c[C_VLP],
+        "shadow queue push": v("queue_push") * c[C_LIGHT],
+        "shadow split rounds: sphere tests": (v("shadow_split:det") + v("shadow_split:roots")) * c[C_SPLIT_IT],
+        "shadow split rounds: rest": v("shadow_split") * c[C_SPLIT],
         "shadow full rounds: det": sh_det * c[C_STEP],
         "shadow full rounds: roots": sh_roots * (c[C_STEP] - c[C_SHSKIP]),
         "shadow full rounds: rest": v("shadow_full") * c[C_FULL],
