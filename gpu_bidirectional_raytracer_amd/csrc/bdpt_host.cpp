@@ -1396,14 +1396,13 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
         else
             HIPCHK(c, hipLaunchKernel(kern, grid, block, kargs, smem, c->stream));
         HIPCHK(c, hipEventRecord(cs.kev[2 * launches + 1], c->stream));
+        const dim3 fgrid((unsigned)((lanes + 255) / 256), 1, 1);   // the fold: 1-D over the launch's rows
         if (st && !unitsl && serial_fold) {                 // the fold after the path kernel
-            grid.z = 1;
-            HIPCHK(c, hipLaunchKernel((const void*)&bdpt_accum_serial_kernel, grid, block, kargs, 0, c->stream));
+            HIPCHK(c, hipLaunchKernel((const void*)&bdpt_accum_serial_kernel, fgrid, block, kargs, 0, c->stream));
         } else if (st && !unitsl) {                         // the ordered fold, on fstream
-            grid.z = 1;
             HIPCHK(c, hipEventRecord(c->rb_path_ev[half], c->stream));
             HIPCHK(c, hipStreamWaitEvent(c->fstream, c->rb_path_ev[half], 0));
-            HIPCHK(c, hipLaunchKernel((const void*)&bdpt_accum_kernel, grid, block, kargs, 0, c->fstream));
+            HIPCHK(c, hipLaunchKernel((const void*)&bdpt_accum_kernel, fgrid, block, kargs, 0, c->fstream));
             HIPCHK(c, hipEventRecord(c->rb_fold_ev[half], c->fstream));
             c->rb_used[half] = true;
             c->fold_last = half;

@@ -1564,24 +1564,19 @@ extern "C" const void* bdpt_path_kernel_table[36] = {BDPT_ROW(false), BDPT_ROW(t
 #undef BDPT_K
 
 // Ordered fold of pass-stream radiance (S > 1): the running mean of device.cu:774-787 applied
-// to rbuf[0..npass) in pass order, so the result is the S == 1 result bit for bit.  Same grid
-// rows (and shard remap) as the path launch; one thread per pixel.
+// to rbuf[0..npass) in pass order, so the result is the S == 1 result bit for bit.  Same rows
+// (and shard remap) as the path launch; one thread per pixel on a 1-D grid over the launch's
+// rows, so a wave reads 768 contiguous bytes per pass (on the path launch's 8x8 wave tiles it
+// read 8 runs of 96 B: caustic8 -1.9 to -3.7 %, cornell S = 64 -0.3 %, weak64 +-0.2 %,
+// profiles/r05_s16_fold_rows_ab.txt).
 template <int U>
 __device__ __forceinline__ void accum_body(const bdpt_path_args& a) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#ifdef BDPT_PROF
-    // section profile (experiments): shader cycles per wave between wave-uniform points, summed
-    // per section and added to a.prof by lane 0 at the end (s_memtime waits on lgkmcnt, so the
-    // profile perturbs LDS overlap a little)
-    unsigned long long pacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pt = __builtin_amdgcn_s_memtime();
-#define BDPT_TICK(k) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); pacc[k] += t_ - pt; pt = t_; } while (0)
-#else
-#define BDPT_TICK(k) do { } while (0)
-#endif
-    const int x = blockIdx.x * BDPT_BTW + (wave % BDPT_BLOCK_WX) * BDPT_WTW + (lane % BDPT_WTW);
-    const int ly = blockIdx.y * BDPT_BTH + (wave / BDPT_BLOCK_WX) * BDPT_WTH + (lane / BDPT_WTW);
-    const int y = bdpt_dev_tile_row(a, blockIdx.y) * BDPT_BTH + (ly - blockIdx.y * BDPT_BTH);
-    if (x >= a.W || y >= a.H) return;
+    const long l = (long)blockIdx.x * 256 + threadIdx.x;
+    if (l >= a.nloc) return;
+    const int ly = (int)(l / a.W);
+    const int x = (int)(l - (long)ly * a.W);
+    const int y = bdpt_dev_tile_row(a, ly / BDPT_BTH) * BDPT_BTH + ly % BDPT_BTH;
+    if (y >= a.H) return;
     if (a.nshards > 1 && ((y / a.band_rows) % a.nshards) != a.shard) return;
     const int i = y * a.W + x;
     const size_t li = (size_t)ly * a.W + x;
