@@ -42,9 +42,11 @@ WORKLOADS = {
 # Per-sample work of each scene, measured once by the CPU restatement over the full 1921x1081
 # frame (tests/test_work_model.py keeps these honest; DESIGN.md "Roofline").
 WORK = {
-    "cornell": {"sphere_tests": 129.4711, "segments": 6.8441, "diffuse": 6.1386, "refr": 0.4528, "rng_reads": 27.0071},
+    "cornell": {"sphere_tests": 129.4711, "segments": 6.8441, "diffuse": 6.1386, "refr": 0.4528, "rng_reads": 27.0071,
+                "_nonzero": 0.9884},
     "cornell_glass": {"sphere_tests": 92.9047, "segments": 6.8374, "diffuse": 4.2323, "refr": 1.02, "rng_reads": 19.9494},
-    "caustic": {"sphere_tests": 5.1332, "segments": 1.5151, "diffuse": 0.4516, "refr": 0.0638, "rng_reads": 3.8704},
+    "caustic": {"sphere_tests": 5.1332, "segments": 1.5151, "diffuse": 0.4516, "refr": 0.0638, "rng_reads": 3.8704,
+                "_nonzero": 0.2160},
     "simple": {"sphere_tests": 8.7195, "segments": 1.5033, "diffuse": 0.5039, "refr": 0.0, "rng_reads": 4.0156},
     "synthetic64": {"sphere_tests": 609.1571, "segments": 6.9145, "diffuse": 5.6567, "refr": 0.908, "rng_reads": 25.5348},
     # large scenes: counted on every 36th row (the full frame takes the oracle a minute)
@@ -634,6 +636,11 @@ def main():
                 # kUnitPasses (8) passes, pixels once per launch; no radiance buffer
                 per_unit = max(1.0, passes_per_launch / 8)          # units of a tile per launch
                 bytes_per_launch = own_pixels * (32 * per_unit + 4) + samples_per_launch * 4 * w["rng_reads"]
+            elif "pixel_pools" in features:
+                # pixel pools: the counter once per pixel; per sample a 1-B mask, and the 12 B of
+                # radiance only when it is not +0 (WORK _nonzero: the oracle's fraction)
+                nz = w.get("_nonzero", 1.0)
+                bytes_per_launch = own_pixels * 4 + samples_per_launch * (4 * w["rng_reads"] + 1 + 12 * nz)
             elif r.last_streams > 1:
                 # pass streams: the path kernel reads the counter once and writes 12 B of radiance
                 # per sample; the fold kernel (not this launch) does the colors/pixels RMW

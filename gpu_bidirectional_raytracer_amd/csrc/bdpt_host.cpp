@@ -130,6 +130,7 @@ struct bdpt_ctx {
     bool last_bvh = false;              // the last path-pass launch traversed the BVH
     int cus = 256;                      // compute units (auto stream count)
     bdpt_dev_vec* d_rbuf = nullptr;     // pass-stream radiance, 2 halves of rbuf_cap: [npass][nloc]
+    unsigned char* d_rmask = nullptr;   // pixel pools: which rbuf samples are stored, same halves
     unsigned* d_poolctr = nullptr;      // pixel pools: claimed pixels per pass and eighth, a line each,
                                         // two sets: a pooled launch uses one and zeroes the other
     int pool_set = 0;                   // the set the next pooled launch uses
@@ -311,7 +312,7 @@ static int upload_scene(bdpt_ctx* c) {
 
 static void release(bdpt_ctx* c) {
     void* bufs[] = {c->d_params, c->d_rand, c->d_rndp, c->d_lp, c->d_sph, c->d_lights, c->d_geom, c->d_lightrec, c->d_colors,
-                    c->d_counter, c->d_pixels, c->d_thr, c->d_rbuf, c->d_poolctr, c->d_uflags, c->d_uerr, c->d_bvh_nodes,
+                    c->d_counter, c->d_pixels, c->d_thr, c->d_rbuf, c->d_rmask, c->d_poolctr, c->d_uflags, c->d_uerr, c->d_bvh_nodes,
                     c->d_bvh_geom, c->d_big_geom, c->d_mat, c->d_bvh_ids, c->d_big_ids,
                     c->d_fcolors, c->d_fcounter, c->d_fpixels, c->d_ftmp, c->d_ftmpc};
     for (void* b : bufs)
@@ -1236,15 +1237,20 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
             HIPCHK(c, hipStreamSynchronize(c->stream));     // queued passes and folds may use it
             HIPCHK(c, hipStreamSynchronize(c->fstream));
             if (c->d_rbuf) HIPCHK(c, hipFree(c->d_rbuf));
+            if (c->d_rmask) HIPCHK(c, hipFree(c->d_rmask));
             c->d_rbuf = nullptr;
+            c->d_rmask = nullptr;
             c->rbuf_cap = 0;
             c->rb_used[0] = c->rb_used[1] = false;
             if (hipMalloc(&c->d_rbuf, 2 * sizeof(bdpt_dev_vec) * need) != hipSuccess)
                 return fail(c, BDPT_ENOMEM, "bdpt_path_passes: pass-stream buffer (2 x %zu B)", sizeof(bdpt_dev_vec) * need);
+            if (hipMalloc(&c->d_rmask, 2 * need) != hipSuccess)
+                return fail(c, BDPT_ENOMEM, "bdpt_path_passes: pass-stream mask (2 x %zu B)", need);
             c->rbuf_cap = need;
             // touch every page now (queued before this call's timing event): the first launch
             // would otherwise pay the first-touch cost, and the stream-mode measurement with it
             HIPCHK(c, hipMemsetAsync(c->d_rbuf, 0, 2 * sizeof(bdpt_dev_vec) * need, c->stream));
+            HIPCHK(c, hipMemsetAsync(c->d_rmask, 0, 2 * need, c->stream));
         }
     }
     const size_t nchunks = grid_rows > 0 ? (size_t)((npass + chunk - 1) / chunk) : 0;
@@ -1266,13 +1272,12 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
         if (st && !jf_pool && !jf_units && !jf_streams) jf_streams = jit_path_kernel(c, true);
         if (!st && !jf_fused) jf_fused = jit_path_kernel(c, false, pair);
     }
-    // Pixel pools fold on the context's stream right after each path kernel (serial fold): the
-    // concurrent fold's HBM traffic slowed the next call's pooled path kernel more than the fold
-    // costs on its own -- caustic pools 4.10 -> 4.04-4.07 ms per call, path kernel 3.93 -> 3.29-3.31
-    // ms; two passes per lane keep the concurrent fold (cornell S = 64 33.82 -> 33.92 ms serial),
-    // profiles/r05_s11_serial_fold.txt.  BDPT_FOLD_SERIAL=0/1 forces either (experiments).
-    static const int fold_env = getenv("BDPT_FOLD_SERIAL") ? atoi(getenv("BDPT_FOLD_SERIAL")) : -1;
-    const bool serial_fold = fold_env >= 0 ? fold_env > 0 : jf_pool != nullptr;
+    // Pixel pools fold on the context's stream right after each path kernel (serial fold, over
+    // their sparse radiance): the concurrent fold's HBM traffic slowed the next call's pooled path
+    // kernel more than the fold costs on its own -- caustic pools 4.10 -> 4.04-4.07 ms per call,
+    // path kernel 3.93 -> 3.29-3.31 ms; two passes per lane keep the concurrent fold (cornell
+    // S = 64 33.82 -> 33.92 ms serial), profiles/r05_s11_serial_fold.txt.
+    const bool serial_fold = jf_pool != nullptr;
     // a fused launch updates colors itself, and a serial fold does so on this stream: they wait
     // for the outstanding concurrent fold, before the call's timing starts (so the stream-mode
     // measurement does not charge that fold to it)
@@ -1324,10 +1329,12 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
             // the units fold in the kernel: no radiance buffer; the previous call's folds were
             // joined above
             a.rbuf = nullptr;
+            a.rmask = nullptr;
         } else if (st) {
             // this half was last read by the fold of the launch before the previous one
             if (c->rb_used[half]) HIPCHK(c, hipStreamWaitEvent(c->stream, c->rb_fold_ev[half], 0));
             a.rbuf = c->d_rbuf + (size_t)half * c->rbuf_cap;
+            a.rmask = c->d_rmask + (size_t)half * c->rbuf_cap;
         } else if (int rc = join_fold(c)) {                  // the fused kernel updates colors itself
             return rc;
         }

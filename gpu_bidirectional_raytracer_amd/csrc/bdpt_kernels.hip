@@ -1410,9 +1410,17 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                     unsigned xyv = xy;
                     asm volatile("" : "+v"(xyv));
                     const int li = kPool ? (int)lix : ((int)(xyv >> 16) - yoff) * a.W + (int)(xyv & 0xffffu);
-                    {
-                    bdpt_dev_vec* rp = a.rbuf + (size_t)(s0 + k * S) * a.nloc + (size_t)li;
-                    *rp = r;
+                    const size_t ri = (size_t)(s0 + k * S) * a.nloc + (size_t)li;
+                    if constexpr (kPool) {
+                        // sparse radiance: pixel pools serve open scenes, where most samples are
+                        // exactly +0 (caustic: 78 % of the samples, half of all 64-pixel runs) --
+                        // a byte marks the stored ones, and the fold reads only those (every bit
+                        // +0 counts as zero, so a -0 component is stored and folded as it is)
+                        const bool nz = (__float_as_uint(r.x) | __float_as_uint(r.y) | __float_as_uint(r.z)) != 0u;
+                        a.rmask[ri] = (unsigned char)nz;
+                        if (nz) a.rbuf[ri] = r;
+                    } else {
+                        a.rbuf[ri] = r;
                     }
                 }
                 fresh = true;
@@ -1569,7 +1577,7 @@ extern "C" const void* bdpt_path_kernel_table[36] = {BDPT_ROW(false), BDPT_ROW(t
 // rows, so a wave reads 768 contiguous bytes per pass (on the path launch's 8x8 wave tiles it
 // read 8 runs of 96 B: caustic8 -1.9 to -3.7 %, cornell S = 64 -0.3 %, weak64 +-0.2 %,
 // profiles/r05_s16_fold_rows_ab.txt).
-template <int U>
+template <int U, bool SPARSE>
 __device__ __forceinline__ void accum_body(const bdpt_path_args& a) {
     const long l = (long)blockIdx.x * 256 + threadIdx.x;
     if (l >= a.nloc) return;
@@ -1587,6 +1595,10 @@ __device__ __forceinline__ void accum_body(const bdpt_path_args& a) {
     const int n = cnt0 >= BDPT_DEV_COUNTER_CAP ? 0
                 : (int)(BDPT_DEV_COUNTER_CAP - cnt0 < (unsigned)a.npass ? BDPT_DEV_COUNTER_CAP - cnt0 : (unsigned)a.npass);
     const bdpt_dev_vec* __restrict__ rb = a.rbuf + li;
+    const unsigned char* __restrict__ rm = a.rmask + li;        // SPARSE: which samples are stored
+    bdpt_dev_vec zero;
+    zero.x = zero.y = zero.z = 0.f;
+    auto sample = [&](int q, bool stored) -> bdpt_dev_vec { return stored ? rb[(size_t)q * a.nloc] : zero; };
     auto fold = [&](const bdpt_dev_vec& r) {
         if (cnt == 0) {
             col = r;
@@ -1605,20 +1617,29 @@ __device__ __forceinline__ void accum_body(const bdpt_path_args& a) {
     if constexpr (U > 1) {                   // U loads in flight (the fold after the path kernel)
         for (; p + U <= n; p += U) {
             bdpt_dev_vec v[U];
+            if constexpr (SPARSE) {
+                unsigned char m[U];
 #pragma unroll
-            for (int u = 0; u < U; u++) v[u] = rb[(size_t)(p + u) * a.nloc];
+                for (int u = 0; u < U; u++) m[u] = rm[(size_t)(p + u) * a.nloc];
+#pragma unroll
+                for (int u = 0; u < U; u++) v[u] = sample(p + u, m[u] != 0);
+            } else {
+#pragma unroll
+                for (int u = 0; u < U; u++) v[u] = sample(p + u, true);
+            }
 #pragma unroll
             for (int u = 0; u < U; u++) fold(v[u]);
         }
     }
-    for (; p < n; p++) fold(rb[(size_t)p * a.nloc]);
+    for (; p < n; p++) fold(sample(p, !SPARSE || rm[(size_t)p * a.nloc] != 0));
     if (cnt == cnt0) return;
     a.colors[i] = col;
     a.counter[i] = cnt;
     a.pixels[i] = bdpt_dev_to_rgba(col.x, col.y, col.z, a.gamma_thr);
 }
-extern "C" __global__ __launch_bounds__(256) void bdpt_accum_kernel(bdpt_path_args a) { accum_body<1>(a); }
-extern "C" __global__ __launch_bounds__(256) void bdpt_accum_serial_kernel(bdpt_path_args a) { accum_body<16>(a); }
+extern "C" __global__ __launch_bounds__(256) void bdpt_accum_kernel(bdpt_path_args a) { accum_body<1, false>(a); }
+// pixel pools: after the path kernel, on its stream, over the sparse radiance
+extern "C" __global__ __launch_bounds__(256) void bdpt_accum_serial_kernel(bdpt_path_args a) { accum_body<16, true>(a); }
 
 // Frame assembly of a multi-device context without RCCL: add a peer's zero-padded frame (exact:
 // each pixel is non-zero on one device only, and x + 0 == x).

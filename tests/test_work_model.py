@@ -25,13 +25,16 @@ def test_work_constants(name):
     step = bench.WORK[name].get("_rows_step", 1)
     st = {}
     for y0, y1 in ([(0, H)] if step == 1 else [(y, y + 1) for y in range(0, H, step)]):
-        _, _, _, s1 = oracle.path_passes(sp, rnd, cam, W, H, lp, sid, vlp, rows=(y0, y1), stats=True)
+        col, _, _, s1 = oracle.path_passes(sp, rnd, cam, W, H, lp, sid, vlp, rows=(y0, y1), stats=True)
         st = {k: st.get(k, 0) + v for k, v in s1.items()}
+        st["nonzero"] = st.get("nonzero", 0) + int((col[y0:y1] != 0).any(axis=2).sum())
     n = st["samples"]
     assert n == W * len(range(0, H, step))
     for k, v in bench.WORK[name].items():
         if k.startswith("_"):
             continue
         assert abs(st[k] / n - v) <= 0.01 * abs(v) + 1e-3, (k, st[k] / n, v)
+    if "_nonzero" in bench.WORK[name]:      # samples whose radiance is not +0 (pools' sparse radiance)
+        assert abs(st["nonzero"] / n - bench.WORK[name]["_nonzero"]) < 2e-4, st["nonzero"] / n
     if name == "cornell":
         assert 3400 < bench.flop_per_sample(bench.WORK["cornell"]) < 3700
