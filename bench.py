@@ -538,13 +538,14 @@ def main():
     r.path_timing(reset=True)
     r.kernel_timing(reset=True)
 
-    # RCCL reduce target: torch tensors over the library's own device buffers (no copy)
+    # frame assembly: torch tensors over the library's own device buffers (no copy); rank 0
+    # gathers every rank's own rows (sharding.gather_frame: RCCL point to point over xGMI)
     t_col = t_cnt = None
     if dist is not None:
         t_col, t_cnt = shd.device_tensors(r, f"cuda:{local}")
-        # one reduce of the same sizes on scratch buffers before the clock starts, so the timed
-        # reduce does not pay RCCL's first-use set-up (channels, buffers) for these sizes
-        shd.reduce_frame(torch.zeros_like(t_col), torch.zeros_like(t_cnt), dst=0)
+        # one gather of the same sizes on scratch buffers before the clock starts, so the timed
+        # one does not pay RCCL's first-use set-up (channels, buffers) for these sizes
+        shd.gather_frame(torch.zeros_like(t_col), torch.zeros_like(t_cnt), W, H, band, dst=0, nshards=nshards)
         torch.cuda.synchronize()
 
     barrier()
@@ -555,7 +556,7 @@ def main():
     r.synchronize()
     t_render = time.perf_counter()                            # rendering done; the reduce is timed apart
     if dist is not None:                                      # assemble the frame on rank 0
-        shd.reduce_frame(t_col, t_cnt, dst=0)
+        shd.gather_frame(t_col, t_cnt, W, H, band, dst=0, nshards=nshards)
     elif mode == "inproc":                                    # in-process RCCL reduce to device 0
         r.reduce_frame()
     torch.cuda.synchronize()
@@ -687,7 +688,8 @@ def main():
                         roofline[{"valu_busy": "valu_busy_pmc",
                                   "valu_lane_utilisation": "lane_utilisation_pmc"}.get(k, k + "_pmc")] = vrec[k]
         if mode == "ranks":
-            reduce_backend = "gloo (torch.distributed, host-staged)" if args.rehearse else "rccl (torch.distributed nccl)"
+            reduce_backend = ("gloo gather (torch.distributed, host-staged)" if args.rehearse
+                              else "rccl gather of owned rows (torch.distributed nccl)")
         elif mode == "inproc":
             reduce_backend = r.reduce_backend + " (in-process bdpt_create_multi)"
         else:

@@ -552,9 +552,10 @@ static int pool_env() {
 // Launch shape of a pooled launch of nloc pixels per pass: {chunk R, grid G}.  One-session probe
 // (profiles/r04_s18_*): caustic 1921 x 1081 best at G = 64, R = 16 on the whole frame; its
 // 1/8 band (260 K pixels) best at G = 16..32, R = 2..4 (fewer waves per pass fill the chip only
-// with smaller G; chunks of G/4 keep ~4 claims per wave).
+// with smaller G; chunks of G/4 keep ~4 claims per wave); with the sparse serial fold, three
+// interleaved rounds put G = 16 3 % ahead of G = 32 there (profiles/r05_s20_pool_grid_n8.txt).
 static void pool_shape(long nloc, int* R, int* G) {
-    int g = nloc >= (1L << 20) ? 64 : (nloc >= (1L << 17) ? 32 : 16);
+    int g = nloc >= (1L << 20) ? 64 : (nloc >= (1L << 19) ? 32 : 16);
     if (const char* e = getenv("BDPT_POOL_GRID")) {
         const int v = atoi(e);
         if (v >= 1) g = v > 256 ? 256 : v;

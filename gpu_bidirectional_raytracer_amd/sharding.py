@@ -3,9 +3,13 @@
 The reference is single-GPU (smallpt_cpu.c:422).  Here every rank renders the rows whose band
 (y // band_rows) is congruent to its rank modulo the world size -- the same rule the path kernel
 applies (bdpt_set_shard) -- and leaves every other pixel at zero.  The only exchange is the
-assembly of the frame: a sum-reduce (torch.distributed, "nccl" = RCCL over xGMI on MI355X, "gloo"
-on CPU) of the float radiance and the counters to one rank, which is exact because each pixel is
-non-zero on exactly one rank (x + 0 == x).
+assembly of the frame on one rank (torch.distributed: "nccl" = RCCL over xGMI on MI355X, "gloo"
+on CPU), in one of two exact forms:
+* gather_frame: every rank packs its own rows (radiance and counter, 16 B per pixel) and the
+  destination receives each peer's 1/N of the frame over that peer's link and copies it into
+  place -- (N-1)/N of one frame into the destination, point to point;
+* reduce_frame: a sum-reduce of the zero-padded frames (each pixel is non-zero on exactly one
+  rank, and x + 0 == x) -- a ring moves about twice the frame over every link.
 """
 from __future__ import annotations
 
@@ -63,3 +67,40 @@ def reduce_frame(t_col, t_cnt, dst: int = 0) -> None:
                 t.copy_(h)
         else:
             dist.reduce(t, dst=dst, op=dist.ReduceOp.SUM)
+
+
+def gather_frame(t_col, t_cnt, width: int, height: int, band_rows: int, dst: int = 0,
+                 nshards: int | None = None) -> None:
+    """Assemble the frame on `dst` from every rank's own rows (exact: copies).  t_col (float32,
+    W*H*3) and t_cnt (int32, W*H) are this rank's zero-padded frame; rank r owns the bands of
+    shard r of `nshards` (default: the world size; weak64's fixed bands: 8); on `dst` the peers'
+    rows are written into them.  One gather of a packed [rows][W*4] int32 buffer per rank (radiance bits
+    and counter side by side, padded to the largest rank's row count); a gloo group with device
+    tensors (multi-rank rehearsals on one GPU) stages it through host memory."""
+    import torch
+    import torch.distributed as dist
+
+    rank, world = dist.get_rank(), dist.get_world_size()
+    rows = [owned_rows(height, r, nshards or world, band_rows) for r in range(world)]
+    m = max(len(x) for x in rows)
+    col2 = t_col.view(height, 3 * width)
+    cnt2 = t_cnt.view(height, width)
+    dev = t_col.device
+    idx = torch.tensor(rows[rank], dtype=torch.long, device=dev)
+    pack = torch.zeros((m, 4 * width), dtype=torch.int32, device=dev)
+    if len(rows[rank]):
+        pack[:len(rows[rank]), :3 * width] = col2.index_select(0, idx).view(torch.int32)
+        pack[:len(rows[rank]), 3 * width:] = cnt2.index_select(0, idx)
+    stage = t_col.is_cuda and dist.get_backend() == "gloo"
+    send = pack.cpu() if stage else pack
+    got = [torch.empty_like(send) for _ in range(world)] if rank == dst else None
+    dist.gather(send, got, dst=dst)
+    if rank != dst:
+        return
+    for r in range(world):
+        if r == dst or not rows[r]:
+            continue                                         # dst's own rows are in place
+        g = got[r].to(dev) if stage else got[r]
+        ri = torch.tensor(rows[r], dtype=torch.long, device=dev)
+        col2.index_copy_(0, ri, g[:len(rows[r]), :3 * width].contiguous().view(torch.float32))
+        cnt2.index_copy_(0, ri, g[:len(rows[r]), 3 * width:].contiguous())
