@@ -82,7 +82,8 @@ struct bdpt_path_args {
     int tiles_per_band;             // > 0: grid rows enumerate only this shard's bands
     int streams;                    // pass streams S: lane (pixel, s) renders passes s, s+S, ...
     bdpt_dev_vec* rbuf;             // S > 1: per (pass, launched pixel) radiance, [npass][nloc]
-    unsigned char* rmask;           // pixel pools: 1 where rbuf holds the sample, 0 = radiance +0 (not stored)
+    unsigned* rmask;                // pixel pools: per launched pixel 4 words, bit p set = rbuf holds
+                                    // pass p's sample (clear: its radiance is +0, not stored)
     int nloc;                       // launched pixels per pass = tile-grid rows * BDPT_BTH * W
     int pool;                       // > 0 (BDPT_POOL builds): a wave renders one pass, restarting lanes
                                     // on new pixels, claimed in chunks of pool x 64 launched pixels

@@ -130,7 +130,7 @@ struct bdpt_ctx {
     bool last_bvh = false;              // the last path-pass launch traversed the BVH
     int cus = 256;                      // compute units (auto stream count)
     bdpt_dev_vec* d_rbuf = nullptr;     // pass-stream radiance, 2 halves of rbuf_cap: [npass][nloc]
-    unsigned char* d_rmask = nullptr;   // pixel pools: which rbuf samples are stored, same halves
+    unsigned* d_rmask = nullptr;        // pixel pools: 4 words per launched pixel (stored passes), 2 halves
     unsigned* d_poolctr = nullptr;      // pixel pools: claimed pixels per pass and eighth, a line each,
                                         // two sets: a pooled launch uses one and zeroes the other
     int pool_set = 0;                   // the set the next pooled launch uses
@@ -146,6 +146,7 @@ struct bdpt_ctx {
     float4 *d_bvh_nodes = nullptr, *d_bvh_geom = nullptr, *d_big_geom = nullptr, *d_mat = nullptr;
     int *d_bvh_ids = nullptr, *d_big_ids = nullptr;
     size_t rbuf_cap = 0;                // elements
+    size_t rmask_lanes = 0;             // launched pixels the mask halves hold (4 words each)
     uint4* d_params = nullptr;          // 4096 x {matrix_a, mask_b, mask_c, seed}
     float* d_rand = nullptr;
     float* d_rndp = nullptr;            // planar copy of d_rand (bdpt_rand_planar_kernel)
@@ -1234,7 +1235,7 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
     if (S > 1 && !want_units) {
         const int cmax = npass < chunk ? npass : chunk;
         const size_t need = (size_t)cmax * (size_t)lanes;
-        if (need > c->rbuf_cap) {
+        if (need > c->rbuf_cap || (size_t)lanes > c->rmask_lanes) {
             HIPCHK(c, hipStreamSynchronize(c->stream));     // queued passes and folds may use it
             HIPCHK(c, hipStreamSynchronize(c->fstream));
             if (c->d_rbuf) HIPCHK(c, hipFree(c->d_rbuf));
@@ -1245,13 +1246,14 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
             c->rb_used[0] = c->rb_used[1] = false;
             if (hipMalloc(&c->d_rbuf, 2 * sizeof(bdpt_dev_vec) * need) != hipSuccess)
                 return fail(c, BDPT_ENOMEM, "bdpt_path_passes: pass-stream buffer (2 x %zu B)", sizeof(bdpt_dev_vec) * need);
-            if (hipMalloc(&c->d_rmask, 2 * need) != hipSuccess)
-                return fail(c, BDPT_ENOMEM, "bdpt_path_passes: pass-stream mask (2 x %zu B)", need);
+            if (hipMalloc(&c->d_rmask, 2 * 16 * (size_t)lanes) != hipSuccess)
+                return fail(c, BDPT_ENOMEM, "bdpt_path_passes: pass-stream mask (2 x %zu B)", 16 * (size_t)lanes);
+            c->rmask_lanes = (size_t)lanes;
             c->rbuf_cap = need;
             // touch every page now (queued before this call's timing event): the first launch
             // would otherwise pay the first-touch cost, and the stream-mode measurement with it
             HIPCHK(c, hipMemsetAsync(c->d_rbuf, 0, 2 * sizeof(bdpt_dev_vec) * need, c->stream));
-            HIPCHK(c, hipMemsetAsync(c->d_rmask, 0, 2 * need, c->stream));
+            HIPCHK(c, hipMemsetAsync(c->d_rmask, 0, 2 * 16 * (size_t)lanes, c->stream));
         }
     }
     const size_t nchunks = grid_rows > 0 ? (size_t)((npass + chunk - 1) / chunk) : 0;
@@ -1335,7 +1337,10 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
             // this half was last read by the fold of the launch before the previous one
             if (c->rb_used[half]) HIPCHK(c, hipStreamWaitEvent(c->stream, c->rb_fold_ev[half], 0));
             a.rbuf = c->d_rbuf + (size_t)half * c->rbuf_cap;
-            a.rmask = c->d_rmask + (size_t)half * c->rbuf_cap;
+            a.rmask = c->d_rmask + (size_t)half * 4 * c->rmask_lanes;
+            // pools mark their stored samples in the mask: cleared first (the fold that read this
+            // half ran earlier on this stream)
+            if (jf_pool) HIPCHK(c, hipMemsetAsync(a.rmask, 0, 16 * (size_t)lanes, c->stream));
         } else if (int rc = join_fold(c)) {                  // the fused kernel updates colors itself
             return rc;
         }

@@ -1414,11 +1414,14 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                     if constexpr (kPool) {
                         // sparse radiance: pixel pools serve open scenes, where most samples are
                         // exactly +0 (caustic: 78 % of the samples, half of all 64-pixel runs) --
-                        // a byte marks the stored ones, and the fold reads only those (every bit
-                        // +0 counts as zero, so a -0 component is stored and folded as it is)
-                        const bool nz = (__float_as_uint(r.x) | __float_as_uint(r.y) | __float_as_uint(r.z)) != 0u;
-                        a.rmask[ri] = (unsigned char)nz;
-                        if (nz) a.rbuf[ri] = r;
+                        // only the others are stored, each marking its pass in the pixel's mask
+                        // (zeroed before the launch), and the fold reads only those (every bit +0
+                        // counts as zero, so a -0 component is stored and folded as it is)
+                        if ((__float_as_uint(r.x) | __float_as_uint(r.y) | __float_as_uint(r.z)) != 0u) {
+                            a.rbuf[ri] = r;
+                            const unsigned pq = (unsigned)(s0 + k * S);
+                            atomicOr(a.rmask + (size_t)li * 4u + (pq >> 5), 1u << (pq & 31u));
+                        }
                     } else {
                         a.rbuf[ri] = r;
                     }
@@ -1595,10 +1598,24 @@ __device__ __forceinline__ void accum_body(const bdpt_path_args& a) {
     const int n = cnt0 >= BDPT_DEV_COUNTER_CAP ? 0
                 : (int)(BDPT_DEV_COUNTER_CAP - cnt0 < (unsigned)a.npass ? BDPT_DEV_COUNTER_CAP - cnt0 : (unsigned)a.npass);
     const bdpt_dev_vec* __restrict__ rb = a.rbuf + li;
-    const unsigned char* __restrict__ rm = a.rmask + li;        // SPARSE: which samples are stored
-    bdpt_dev_vec zero;
-    zero.x = zero.y = zero.z = 0.f;
-    auto sample = [&](int q, bool stored) -> bdpt_dev_vec { return stored ? rb[(size_t)q * a.nloc] : zero; };
+    unsigned m0 = 0u, m1 = 0u, m2 = 0u, m3 = 0u;                 // SPARSE: which passes are stored
+    if constexpr (SPARSE) {
+        const uint4 mw = reinterpret_cast<const uint4*>(a.rmask)[li];
+        m0 = mw.x; m1 = mw.y; m2 = mw.z; m3 = mw.w;
+    }
+    // (the load under a branch, component by component: `stored ? rb[q] : zero` on the struct
+    // became a load through a selected pointer, with `zero` on the stack)
+    auto sample = [&](int q, bool stored) -> bdpt_dev_vec {
+        bdpt_dev_vec v;
+        v.x = v.y = v.z = 0.f;
+        if (stored) {
+            const bdpt_dev_vec* e = rb + (size_t)q * a.nloc;
+            v.x = e->x;
+            v.y = e->y;
+            v.z = e->z;
+        }
+        return v;
+    };
     auto fold = [&](const bdpt_dev_vec& r) {
         if (cnt == 0) {
             col = r;
@@ -1618,11 +1635,10 @@ __device__ __forceinline__ void accum_body(const bdpt_path_args& a) {
         for (; p + U <= n; p += U) {
             bdpt_dev_vec v[U];
             if constexpr (SPARSE) {
-                unsigned char m[U];
+                const unsigned w = p < 64 ? (p < 32 ? m0 : m1) : (p < 96 ? m2 : m3);
+                const unsigned bits = w >> (p & 31);              // p is a multiple of U = 16
 #pragma unroll
-                for (int u = 0; u < U; u++) m[u] = rm[(size_t)(p + u) * a.nloc];
-#pragma unroll
-                for (int u = 0; u < U; u++) v[u] = sample(p + u, m[u] != 0);
+                for (int u = 0; u < U; u++) v[u] = sample(p + u, (bits >> u) & 1u);
             } else {
 #pragma unroll
                 for (int u = 0; u < U; u++) v[u] = sample(p + u, true);
@@ -1631,7 +1647,10 @@ __device__ __forceinline__ void accum_body(const bdpt_path_args& a) {
             for (int u = 0; u < U; u++) fold(v[u]);
         }
     }
-    for (; p < n; p++) fold(sample(p, !SPARSE || rm[(size_t)p * a.nloc] != 0));
+    for (; p < n; p++) {
+        const unsigned w = p < 64 ? (p < 32 ? m0 : m1) : (p < 96 ? m2 : m3);
+        fold(sample(p, !SPARSE || ((w >> (p & 31)) & 1u)));
+    }
     if (cnt == cnt0) return;
     a.colors[i] = col;
     a.counter[i] = cnt;
