@@ -69,7 +69,8 @@ def sections():
     split_end = find(r"continue;", split)
     t3 = find(r"BDPT_TICK\(3\)", split_end)
     t4 = find(r"BDPT_TICK\(4\)", t3)
-    regen = find(r"if constexpr \(kRegen\) \{", find(r"if constexpr \(kPool\) \{", t4))
+    pool = find(r"// lanes whose path ended take the next pixels", t4) - 1      # its `if constexpr (kPool)`
+    regen = find(r"// release the parked lanes together", pool) - 1
     t5 = find(r"BDPT_TICK\(5\)", regen)
     end = find(r"^}", t5)
     return [("prologue", k0, loop - 1), ("loop_control", loop, cam - 1), ("camera", cam, ch - 1),
@@ -78,13 +79,13 @@ def sections():
             ("fresnel", fres, fres_end), ("next_direction", dirb, blk_end),
             ("shading", blk_end + 1, t1), ("nee_setup", t1 + 1, vlp_in), ("vlp_setup", vlp_in + 1, vlp_end - 1),
             ("queue_push", vlp_end, t2), ("shadow_split", split, split_end),
-            ("shadow_full", t2 + 1, t3), ("shadow_results", t3 + 1, t4), ("path_end", t4 + 1, regen - 1),
+            ("shadow_full", t2 + 1, t3), ("shadow_results", t3 + 1, t4), ("path_end", t4 + 1, pool - 1), ("pool_claim", pool, regen - 1),
             ("regen_release", regen, t5), ("epilogue", t5 + 1, end)], (k0, end)
 
 
-def static_counts(scene, units, keep=None):
+def static_counts(scene, units, keep=None, pool=False):
     secs, (k0, kend) = sections()
-    extra = ["-gline-tables-only"] + (["-DBDPT_UNITS=1"] if units else [])
+    extra = ["-gline-tables-only"] + (["-DBDPT_UNITS=1"] if units else []) + (["-DBDPT_POOL=1"] if pool else [])
     with tempfile.TemporaryDirectory() as tmp:
         wd = keep or tmp
         os.makedirs(wd, exist_ok=True)
@@ -192,6 +193,7 @@ def attribute(cnt, c, n_spheres, n_small):
         "shadow results + contribution": v("shadow_results") * c[C_LIGHT],
         "path end / accumulation / RNG loads": v("path_end") * c[C_ITER],
         "regen release": v("regen_release") * c[C_REGEN],
+        "pool claim + next pixel set-up (pools)": v("pool_claim") * c[C_ITER],
     }
     # per path in the PMC's sense: wave instructions per 64 paths (a wave instruction serves 64
     # lanes; scripts/pmc_summary.py valu_insts_per_wave = SQ_INSTS_VALU / SQ_WAVES, over the
@@ -211,11 +213,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("scene", nargs="?", default=os.path.join(REPO, "assets", "scenes", "cornell.scn"))
     ap.add_argument("--units", action="store_true", help="the in-kernel fold build (-DBDPT_UNITS=1)")
+    ap.add_argument("--pool", action="store_true", help="the pixel-pool build (-DBDPT_POOL=1)")
     ap.add_argument("--counts", help="file holding a bdpt_counts line")
     ap.add_argument("--pmc-valu", type=float, help="measured SQ_INSTS_VALU per wave and path per lane")
     ap.add_argument("--keep")
     args = ap.parse_args()
-    cnt = static_counts(args.scene, args.units, args.keep)
+    cnt = static_counts(args.scene, args.units, args.keep, args.pool)
     if not args.counts:
         print(json.dumps({f"{s}/{c}": n for (s, c), n in sorted(cnt.items())}, indent=1))
         return 0
