@@ -76,3 +76,47 @@ def test_pool_shard_matches_oracle(gpu, rnd0, band, monkeypatch):
     owned = (np.arange(H) // band) % N == rank
     assert (cnt[owned] == npass).all() and (cnt[~owned] == 0).all() and (col[~owned] == 0).all()
     assert np.array_equal(col[owned].view(np.uint32), ocol[owned].view(np.uint32))
+
+
+@pytest.mark.parametrize("name", ["caustic", "cornell"])
+def test_pool_long_call_sparse_fold(gpu, rnd0, name, monkeypatch):
+    """One call of 200 passes = two pooled launches of 100 (all four mask words of a pixel, and a
+    fold tail of 100 mod 16 passes); caustic's samples are mostly +0 (sparse radiance)."""
+    monkeypatch.setenv("BDPT_POOL", "4")
+    W, H, npass = 31, 17, 200
+    s = g.PassScheduler()
+    s.light()
+    sid, vlp = s.next(npass)
+    cam, sp = g.read_scene(os.path.join(SCENES, name + ".scn"))
+    g.update_camera(cam, W, H)
+    with g.Renderer(sp, W, H, cam, device=0) as r:
+        r.set_streams(128)
+        r.light_pass(0)
+        r.path_passes(sid, vlp)
+        assert "pixel_pools" in r.last_features, r.last_features
+        col, cnt = r.read_radiance()
+    ocol, ocnt, _ = _oracle(name, W, H, sid, vlp, rnd0)
+    assert np.array_equal(cnt, ocnt)
+    assert np.array_equal(col.view(np.uint32), ocol.view(np.uint32))
+
+
+def test_pool_counter_cap(gpu, rnd0, monkeypatch):
+    """Pooled launches across the 30000-pass counter cap: passes past it are neither rendered nor
+    folded (their mask bits stay clear and the fold stops at the cap)."""
+    monkeypatch.setenv("BDPT_POOL", "4")
+    W, H = 5, 3
+    s = g.PassScheduler()
+    s.light()
+    sid, vlp = s.next(30004)
+    cam, sp = g.read_scene(os.path.join(SCENES, "caustic.scn"))
+    g.update_camera(cam, W, H)
+    with g.Renderer(sp, W, H, cam, device=0) as r:
+        r.set_streams(128)
+        r.light_pass(0)
+        r.path_passes(sid[:29950], vlp[:29950])
+        r.path_passes(sid[29950:], vlp[29950:])               # the cap falls inside this call
+        assert "pixel_pools" in r.last_features, r.last_features
+        col, cnt = r.read_radiance()
+    assert (cnt == 30000).all()
+    ocol, ocnt, _ = _oracle("caustic", W, H, sid, vlp, rnd0)
+    assert np.array_equal(col.view(np.uint32), ocol.view(np.uint32))
