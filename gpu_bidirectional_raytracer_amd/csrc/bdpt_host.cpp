@@ -56,10 +56,11 @@ struct bdpt_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     // Pass-stream folds (bdpt_accum_kernel) run on their own stream so that a launch's fold
-    // overlaps the next launch's path kernel (VALU-bound; the fold is a memory stream).  The
+    // overlaps the next launch's path kernel (VALU-bound; the fold is a memory stream); pixel
+    // pools fold on `stream` right after their launch instead (bdpt_accum_serial_kernel).  The
     // radiance buffer is double-buffered: launch L writes half L % 2 after the fold of launch L-2
     // has read it.  Everything else that touches colors/counter/pixels runs on `stream` after
-    // join_fold() has made it wait for the last fold.
+    // join_fold() has made it wait for the last concurrent fold.
     hipStream_t fstream = nullptr;
     unsigned long long* d_prof = nullptr;   // BDPT_PROF=1 (with a -DBDPT_PROF kernel): section cycles
     hipEvent_t rb_path_ev[2] = {nullptr, nullptr};   // path kernel of the half done (stream)

@@ -1,0 +1,141 @@
+#!/bin/bash
+# The round-5 GPU sessions whose results are under profiles/r05_s<N>_* (one function per
+# session; each ran as `gpurun -- bash scripts/r05_sessions.sh s<N>`).  Later rounds: use
+# scripts/ab.sh for A/Bs and add a session here only when its output is committed.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; mkdir -p gpurun_out; export TMPDIR=/tmp
+
+s9() {
+  # round 5 session 9: per-workload rocprof stats + PMC records (units for cornell1080), weak64 bench
+  cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+  mkdir -p gpurun_out
+  export TMPDIR=/tmp
+  WORKLOADS="cornell1080:64:cornell1080:BDPT_UNITS=8 caustic8:128:caustic8:BDPT_POOL=16 weak64:32" bash scripts/profile_workloads.sh
+}
+
+s10() {
+  timeout -k 10 300 python -u -m pytest tests/test_gpu_units.py tests/test_gpu_parity.py -k "units or auto_streams" -x -q --timeout 120 --timeout-method thread > gpurun_out/s10_pytest.log 2>&1 || { tail -20 gpurun_out/s10_pytest.log; exit 1; }
+  tail -2 gpurun_out/s10_pytest.log
+  NS="2 4" WORKLOADS="cornell1080" STEPS_N=4 bash scripts/rehearse.sh || exit 1
+  for n in 2 4; do grep '^{' gpurun_out/rehearse_cornell1080_$n.log | tail -1 > gpurun_out/s10_rehearse_$n.json; done
+  timeout -k 10 300 python bench.py --gpus 2 --devices 0,0 --steps 5 --no-cpu-baseline > gpurun_out/s10_inproc.log 2>&1 || { tail -20 gpurun_out/s10_inproc.log; exit 1; }
+  grep '^{' gpurun_out/s10_inproc.log | tail -1 > gpurun_out/s10_inproc.json
+  for f in gpurun_out/s10_rehearse_2.json gpurun_out/s10_rehearse_4.json gpurun_out/s10_inproc.json; do
+  python3 -c "
+  import json; d=json.load(open('$f'))
+  print('$f', d['n_gpus'], d['value'], d['reduce_backend'], 'fallback', d.get('reduce_fallback'), 'choice_from', d.get('stream_choice_from'))
+  for p in d['scaling_breakdown']['per_device']: print('   ', p.get('rank', p.get('device')), p['mode'])"
+  done
+  timeout -k 10 120 python scripts/probe_step.py --scene cornell --streams 64 --tag units8 > gpurun_out/s10_probe.txt 2>&1 && BDPT_UNITS=8 timeout -k 10 120 python scripts/probe_step.py --scene cornell --streams 64 --tag units8 >> gpurun_out/s10_probe.txt 2>&1; grep '^{' gpurun_out/s10_probe.txt | cut -c1-150
+}
+
+s11() {
+  ARGS="--scene caustic --streams 128" ROUNDS=2 VARIANTS="pools:BDPT_POOL=16 pools_serial:BDPT_POOL=16;BDPT_FOLD_SERIAL=1 pools_m16:BDPT_POOL=16;BDPT_MAX_LAUNCH_PASSES=16 pools_m8:BDPT_POOL=16;BDPT_MAX_LAUNCH_PASSES=8" OUT=gpurun_out/s11_serial.txt bash scripts/ab.sh || exit 1
+  ARGS="--scene cornell --streams 64" ROUNDS=2 VARIANTS="s64: s64_serial:BDPT_FOLD_SERIAL=1" OUT=gpurun_out/s11_serial.txt bash scripts/ab.sh || exit 1
+  BDPT_UNITS=8 BDPT_PROF=counts BDPT_JIT_FLAGS=-DBDPT_COUNTS=1 timeout -k 10 150 python scripts/probe_step.py --scene cornell --streams 64 --reps 2 --tag counts_units > gpurun_out/s11_counts_units.txt 2>&1 || exit 1
+  BDPT_PROF=counts BDPT_JIT_FLAGS=-DBDPT_COUNTS=1 timeout -k 10 150 python scripts/probe_step.py --scene cornell --streams 64 --reps 2 --tag counts_s64 > gpurun_out/s11_counts_s64.txt 2>&1 || exit 1
+  grep -h "bdpt_counts\|^{" gpurun_out/s11_counts_*.txt | cut -c1-200
+}
+
+s12() {
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "pool or auto or stream or fold or caustic" > gpurun_out/s12_pytest.log 2>&1 || { tail -30 gpurun_out/s12_pytest.log; exit 1; }
+  tail -3 gpurun_out/s12_pytest.log
+  MODE=bench ARGS="--workload caustic8 --no-cpu-baseline --steps 20" ROUNDS=2 VARIANTS="serial: concurrent:BDPT_FOLD_SERIAL=0" OUT=gpurun_out/s12_bench.txt bash scripts/ab.sh || exit 1
+  timeout -k 10 400 python scripts/shard_probe.py --scene caustic --passes 128 --strong --reps 3 > gpurun_out/s12_caustic_strong.txt 2>&1 || { tail -20 gpurun_out/s12_caustic_strong.txt; exit 1; }
+  tail -12 gpurun_out/s12_caustic_strong.txt
+}
+
+s13() {
+  timeout -k 10 500 python scripts/shard_probe.py --scene caustic --passes 128 --strong --reps 20 > gpurun_out/s13_caustic_strong.txt 2>&1 || { tail -20 gpurun_out/s13_caustic_strong.txt; exit 1; }
+  tail -8 gpurun_out/s13_caustic_strong.txt
+}
+
+s14() {
+  BDPT_UNITS=8 BDPT_PROF=counts BDPT_JIT_FLAGS=-DBDPT_COUNTS=1 timeout -k 10 200 python scripts/probe_step.py --scene cornell --streams 64 --reps 2 --tag counts_units > gpurun_out/s14_counts_units.txt 2>&1 || { tail -20 gpurun_out/s14_counts_units.txt; exit 1; }
+  grep -h "bdpt_counts" gpurun_out/s14_counts_units.txt
+  timeout -k 10 500 python scripts/shard_probe.py --scene caustic --passes 128 --strong --reps 20 > gpurun_out/s14_caustic_strong.txt 2>&1 || { tail -20 gpurun_out/s14_caustic_strong.txt; exit 1; }
+  tail -8 gpurun_out/s14_caustic_strong.txt
+}
+
+s16() {
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "pool or auto or stream or fold or caustic or shard" > gpurun_out/s16_pytest.log 2>&1 || { tail -30 gpurun_out/s16_pytest.log; exit 1; }
+  tail -2 gpurun_out/s16_pytest.log
+  BDPT_FOLD_ROWS=1 timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "stream and not pool" > gpurun_out/s16_pytest_rows.log 2>&1 || { tail -30 gpurun_out/s16_pytest_rows.log; exit 1; }
+  tail -2 gpurun_out/s16_pytest_rows.log
+  MODE=bench ARGS="--workload caustic8 --no-cpu-baseline --steps 20" ROUNDS=2 VARIANTS="rows: tiles:BDPT_FOLD_ROWS=0" OUT=gpurun_out/s16_ab.txt bash scripts/ab.sh || exit 1
+  ARGS="--scene cornell --streams 64" ROUNDS=2 VARIANTS="s64: s64rows:BDPT_FOLD_ROWS=1" OUT=gpurun_out/s16_ab.txt bash scripts/ab.sh || exit 1
+  MODE=bench ARGS="--workload weak64 --no-cpu-baseline --steps 6" ROUNDS=2 VARIANTS="w64: w64rows:BDPT_FOLD_ROWS=1" OUT=gpurun_out/s16_ab.txt bash scripts/ab.sh || exit 1
+}
+
+s17() {
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/s17_pytest.log 2>&1 || { tail -30 gpurun_out/s17_pytest.log; exit 1; }
+  tail -2 gpurun_out/s17_pytest.log
+  timeout -k 10 300 python bench.py --workload caustic8 > gpurun_out/s17_bench_caustic8.json 2> gpurun_out/s17_bench_caustic8.err || exit 1
+  tail -1 gpurun_out/s17_bench_caustic8.json | cut -c1-400
+  timeout -k 10 400 python bench.py > gpurun_out/s17_bench.json 2> gpurun_out/s17_bench.err || exit 1
+  tail -1 gpurun_out/s17_bench.json | cut -c1-400
+}
+
+s18() {
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "pool or auto or stream or fold or caustic or shard or config" > gpurun_out/s18_pytest.log 2>&1 || { tail -30 gpurun_out/s18_pytest.log; exit 1; }
+  tail -2 gpurun_out/s18_pytest.log
+  MODE=bench ARGS="--workload caustic8 --no-cpu-baseline --steps 20" ROUNDS=3 VARIANTS="sparse:" OUT=gpurun_out/s18_ab.txt bash scripts/ab.sh || exit 1
+  timeout -k 10 500 python scripts/shard_probe.py --scene caustic --passes 128 --strong --reps 20 --ns 1,8 > gpurun_out/s18_caustic_strong.txt 2>&1 || { tail -20 gpurun_out/s18_caustic_strong.txt; exit 1; }
+  tail -4 gpurun_out/s18_caustic_strong.txt
+}
+
+s19() {
+  for v in "base:" "g16r4:BDPT_POOL_GRID=16;BDPT_POOL=4" "g16r2:BDPT_POOL_GRID=16;BDPT_POOL=2" "g8r2:BDPT_POOL_GRID=8;BDPT_POOL=2" "g64r8:BDPT_POOL_GRID=64;BDPT_POOL=8" "g32r4:BDPT_POOL_GRID=32;BDPT_POOL=4"; do
+    tag=${v%%:*}; envs=${v#*:}; IFS=';' read -r -a assign <<< "$envs"
+    env "${assign[@]}" timeout -k 10 200 python scripts/shard_probe.py --scene caustic --passes 128 --strong --reps 20 --ns 8 > gpurun_out/s19_$tag.txt 2>&1 || { tail -5 gpurun_out/s19_$tag.txt; exit 1; }
+    echo "$tag $(grep '"streams_req": 0' gpurun_out/s19_$tag.txt | tail -1)" | tee -a gpurun_out/s19_grid.txt
+  done
+}
+
+s20() {
+  for r in 1 2 3; do
+  for v in "base:" "g16r4:BDPT_POOL_GRID=16;BDPT_POOL=4" "g64r8:BDPT_POOL_GRID=64;BDPT_POOL=8" "g128r16:BDPT_POOL_GRID=128;BDPT_POOL=16" "g64r16:BDPT_POOL_GRID=64;BDPT_POOL=16"; do
+    tag=${v%%:*}; envs=${v#*:}; IFS=';' read -r -a assign <<< "$envs"
+    env "${assign[@]}" timeout -k 10 200 python scripts/shard_probe.py --scene caustic --passes 128 --strong --reps 30 --ns 8 > gpurun_out/s20_$tag.txt 2>&1 || { tail -5 gpurun_out/s20_$tag.txt; exit 1; }
+    echo "$r $tag $(grep '"streams_req": 0' gpurun_out/s20_$tag.txt | tail -1)" | tee -a gpurun_out/s20_grid.txt
+  done
+  done
+}
+
+s21() {
+  timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "pool" > gpurun_out/s21_pytest.log 2>&1 || { tail -30 gpurun_out/s21_pytest.log; exit 1; }
+  tail -1 gpurun_out/s21_pytest.log
+  timeout -k 10 500 python scripts/shard_probe.py --scene caustic --passes 128 --strong --reps 30 > gpurun_out/s21_caustic_strong.txt 2>&1 || { tail -20 gpurun_out/s21_caustic_strong.txt; exit 1; }
+  grep '"streams_req": 0' gpurun_out/s21_caustic_strong.txt
+  timeout -k 10 500 python scripts/shard_probe.py --scene caustic --passes 128 --strong --reps 30 > gpurun_out/s21_caustic_strong2.txt 2>&1 || { tail -20 gpurun_out/s21_caustic_strong2.txt; exit 1; }
+  grep '"streams_req": 0' gpurun_out/s21_caustic_strong2.txt
+}
+
+s22() {
+  NS="2 4" WORKLOADS="caustic8 cornell1080" STEPS_N=4 bash scripts/rehearse.sh || exit 1
+  NS="2" WORKLOADS="weak64" STEPS_N=2 bash scripts/rehearse.sh || exit 1
+  for f in gpurun_out/rehearse_caustic8_2.log gpurun_out/rehearse_caustic8_4.log gpurun_out/rehearse_cornell1080_2.log gpurun_out/rehearse_cornell1080_4.log gpurun_out/rehearse_weak64_2.log; do
+  grep '^{' $f | tail -1 | python3 -c "
+  import json,sys; d=json.loads(sys.stdin.read())
+  sb=d['scaling_breakdown']
+  print('$f', d['n_gpus'], d['value'], d['reduce_backend'], 'render', sb['render_s'], 'reduce', sb['reduce_s'])"
+  done
+}
+
+s23() {
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "pool or auto or stream or fold or caustic or shard or config" > gpurun_out/s23_pytest.log 2>&1 || { tail -30 gpurun_out/s23_pytest.log; exit 1; }
+  tail -1 gpurun_out/s23_pytest.log
+  MODE=bench ARGS="--workload caustic8 --no-cpu-baseline --steps 20" ROUNDS=3 VARIANTS="bits:" OUT=gpurun_out/s23_ab.txt bash scripts/ab.sh || exit 1
+  rm -rf gpurun_out/prof_s23 && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_s23 -o run --output-format csv -- python3 bench.py --workload caustic8 --no-cpu-baseline --steps 10 > gpurun_out/prof_s23.log 2>&1 || exit 1
+  head -4 gpurun_out/prof_s23/run_kernel_stats.csv | cut -c1-150
+}
+
+s24() {
+  BDPT_POOL=16 BDPT_PROF=counts BDPT_JIT_FLAGS=-DBDPT_COUNTS=1 timeout -k 10 200 python scripts/probe_step.py --scene caustic --streams 128 --reps 2 --tag counts_pools > gpurun_out/s24_counts_pools.txt 2>&1 || { tail -20 gpurun_out/s24_counts_pools.txt; exit 1; }
+  grep -h "bdpt_counts" gpurun_out/s24_counts_pools.txt
+}
+
+case "${1:-}" in
+  s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24) "$1" ;;
+  *) echo "usage: $0 {s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24}"; exit 2 ;;
+esac
