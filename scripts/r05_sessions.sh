@@ -135,7 +135,11 @@ s24() {
   grep -h "bdpt_counts" gpurun_out/s24_counts_pools.txt
 }
 
+s27() {
+  MODE=bench ARGS="--workload caustic8 --no-cpu-baseline --steps 20" ROUNDS=3 VARIANTS="u16: u8:BDPT_FOLD_U=8 u32:BDPT_FOLD_U=32" OUT=gpurun_out/s27_fold_u.txt bash scripts/ab.sh || exit 1
+}
+
 case "${1:-}" in
-  s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24) "$1" ;;
-  *) echo "usage: $0 {s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24}"; exit 2 ;;
+  s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27) "$1" ;;
+  *) echo "usage: $0 {s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27}"; exit 2 ;;
 esac
