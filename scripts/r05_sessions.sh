@@ -139,7 +139,18 @@ s27() {
   MODE=bench ARGS="--workload caustic8 --no-cpu-baseline --steps 20" ROUNDS=3 VARIANTS="u16: u8:BDPT_FOLD_U=8 u32:BDPT_FOLD_U=32" OUT=gpurun_out/s27_fold_u.txt bash scripts/ab.sh || exit 1
 }
 
+s28() {
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/s28_pytest.log 2>&1 || { tail -30 gpurun_out/s28_pytest.log; exit 1; }
+  tail -1 gpurun_out/s28_pytest.log
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/s28_smoke.log 2>&1 || { tail -20 gpurun_out/s28_smoke.log; exit 1; }
+  tail -1 gpurun_out/s28_smoke.log
+  timeout -k 10 400 python bench.py > gpurun_out/s28_bench.json 2> gpurun_out/s28_bench.err || exit 1
+  timeout -k 10 300 python bench.py --workload caustic8 > gpurun_out/s28_bench_caustic8.json 2> gpurun_out/s28_bench_caustic8.err || exit 1
+  timeout -k 10 400 python bench.py --workload weak64 > gpurun_out/s28_bench_weak64.json 2> gpurun_out/s28_bench_weak64.err || exit 1
+  for f in s28_bench s28_bench_caustic8 s28_bench_weak64; do tail -1 gpurun_out/$f.json | cut -c1-120; done
+}
+
 case "${1:-}" in
-  s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27) "$1" ;;
-  *) echo "usage: $0 {s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27}"; exit 2 ;;
+  s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28) "$1" ;;
+  *) echo "usage: $0 {s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28}"; exit 2 ;;
 esac
