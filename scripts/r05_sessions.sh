@@ -150,7 +150,14 @@ s28() {
   for f in s28_bench s28_bench_caustic8 s28_bench_weak64; do tail -1 gpurun_out/$f.json | cut -c1-120; done
 }
 
+s29() {
+  timeout -k 10 900 python scripts/shard_probe.py --scene cornell --passes 128 --reps 3 > gpurun_out/s29_cornell_weak.txt 2>&1 || { tail -20 gpurun_out/s29_cornell_weak.txt; exit 1; }
+  grep '"streams_req": 0' gpurun_out/s29_cornell_weak.txt
+  timeout -k 10 900 python scripts/shard_probe.py --workload weak64 --reps 2 > gpurun_out/s29_weak64_bands.txt 2>&1 || { tail -20 gpurun_out/s29_weak64_bands.txt; exit 1; }
+  tail -1 gpurun_out/s29_weak64_bands.txt
+}
+
 case "${1:-}" in
-  s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28) "$1" ;;
-  *) echo "usage: $0 {s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28}"; exit 2 ;;
+  s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29) "$1" ;;
+  *) echo "usage: $0 {s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29}"; exit 2 ;;
 esac
