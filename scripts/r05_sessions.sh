@@ -157,7 +157,11 @@ s29() {
   tail -1 gpurun_out/s29_weak64_bands.txt
 }
 
+s30() {
+  ARGS="--scene synthetic64 --width 4097 --height 513 --streams 64" ROUNDS=2 VARIANTS="s64: units8:BDPT_UNITS=8 units16:BDPT_UNITS=16 pools:BDPT_POOL=16" OUT=gpurun_out/s30_weak64_modes.txt LIMIT=300 bash scripts/ab.sh || exit 1
+}
+
 case "${1:-}" in
-  s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29) "$1" ;;
-  *) echo "usage: $0 {s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29}"; exit 2 ;;
+  s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29|s30) "$1" ;;
+  *) echo "usage: $0 {s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29|s30}"; exit 2 ;;
 esac
