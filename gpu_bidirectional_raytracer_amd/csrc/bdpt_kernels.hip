@@ -695,6 +695,30 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
             G[s] = make_float4(S.px, S.py, S.pz, S.rr);
         }
     }
+    // pixel pools: a workgroup whose pass was drained before it started ends at once (a launch
+    // has many more workgroups than fit, and the late ones of a pass find it drained): threads
+    // 0..7 read the pass's 8 claim counters in parallel (the claim would try them one after
+    // another); the pass is drained when every part is.  caustic +0.3 %, its 1/8 share +1.3 %
+    // (profiles/r05_s33_pool_early_exit.txt); a "drained" bitmap instead -- one word for 32
+    // passes, set by every wave whose claim failed -- was a contended hot spot (-30 %,
+    // r05_s32_pool_skip_bitmap.txt).
+    __shared__ unsigned pool_left;
+    if constexpr (kPool) {
+        // the next pooled launch's counters (the previous launch used them and has finished);
+        // before the early exit, so every workgroup does its share
+        for (unsigned w = blockIdx.x * 256u + threadIdx.x; w < 128u * 8u; w += gridDim.x * 256u)
+            a.pool_ctr_next[w * 32u] = 0u;
+    }
+    if (kPool && threadIdx.x == 0) pool_left = 0u;
+    __syncthreads();
+    if (kPool && threadIdx.x < 8u) {
+        const unsigned nl = (unsigned)a.nloc, pt = threadIdx.x;
+        const unsigned p0 = (unsigned)(((unsigned long long)nl * pt) >> 3);
+        const unsigned p1 = (unsigned)(((unsigned long long)nl * (pt + 1u)) >> 3);
+        const unsigned used = __hip_atomic_load(a.pool_ctr + ((unsigned)s0 * 8u + pt) * 32u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+        if (p0 + used < p1) atomicOr(&pool_left, 1u);                // LDS
+    }
     for (int q = threadIdx.x; q < nslot; q += 256) {
         const int pq = s0 + q * S;
         const bool inl = a.sid == nullptr;                                // uniform
@@ -723,6 +747,7 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
         sct[q + threadIdx.x] = bdpt_sincos_table_dev[(q + threadIdx.x) << BDPT_SC_COARSE][0];
     const double* SCT = sct;
     __syncthreads();
+    if (kPool && pool_left == 0u) return;                // uniform: the whole workgroup ends
 
     auto geom = [&](int s) -> float4 {
 #ifdef BDPT_JIT
@@ -841,9 +866,6 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
         return a.nshards <= 1 || a.tiles_per_band > 0 || ((py / a.band_rows) % a.nshards) == a.shard;
     };
     if constexpr (kPool) {
-        // the next pooled launch's counters (the previous launch used them and has finished)
-        for (unsigned w = blockIdx.x * 256u + threadIdx.x; w < 128u * 8u; w += gridDim.x * 256u)
-            a.pool_ctr_next[w * 32u] = 0u;
         active = claim();
         lix = pcur + (unsigned)lane;
         pcur += 64u;

@@ -161,7 +161,43 @@ s30() {
   ARGS="--scene synthetic64 --width 4097 --height 513 --streams 64" ROUNDS=2 VARIANTS="s64: units8:BDPT_UNITS=8 units16:BDPT_UNITS=16 pools:BDPT_POOL=16" OUT=gpurun_out/s30_weak64_modes.txt LIMIT=300 bash scripts/ab.sh || exit 1
 }
 
+s31() {
+  timeout -k 10 300 python -u -m pytest tests/test_gpu_pool.py tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k "pool or auto" > gpurun_out/s31_pytest.log 2>&1 || { tail -30 gpurun_out/s31_pytest.log; exit 1; }
+  tail -1 gpurun_out/s31_pytest.log
+  MODE=bench ARGS="--workload caustic8 --no-cpu-baseline --steps 20" ROUNDS=2 VARIANTS="skip: noskip:BDPT_JIT_FLAGS=-DBDPT_POOL_NOSKIP=1" OUT=gpurun_out/s31_ab.txt bash scripts/ab.sh || exit 1
+  for r in 1 2; do for v in "skip:" "noskip:BDPT_JIT_FLAGS=-DBDPT_POOL_NOSKIP=1"; do
+    tag=${v%%:*}; envs=${v#*:}; IFS=';' read -r -a assign <<< "$envs"
+    env "${assign[@]}" timeout -k 10 200 python scripts/shard_probe.py --scene caustic --passes 128 --strong --reps 30 --ns 1,8 > gpurun_out/s31_$tag.txt 2>&1 || { tail -5 gpurun_out/s31_$tag.txt; exit 1; }
+    echo "$r $tag $(grep '"streams_req": 0' gpurun_out/s31_$tag.txt | tr '\n' ' ')" | tee -a gpurun_out/s31_n8.txt
+  done; done
+}
+
+s32() {
+  for r in 1 2; do for v in "skip:BDPT_POOL=16" "noskip:BDPT_POOL=16;BDPT_JIT_FLAGS=-DBDPT_POOL_NOSKIP=1"; do
+    tag=${v%%:*}; envs=${v#*:}; IFS=';' read -r -a assign <<< "$envs"
+    env "${assign[@]}" timeout -k 10 200 python scripts/probe_step.py --scene caustic --streams 128 --reps 10 --tag $tag > gpurun_out/s32_n1_$tag.txt 2>&1 || { tail -5 gpurun_out/s32_n1_$tag.txt; exit 1; }
+    echo "$r N1 $(grep '^{' gpurun_out/s32_n1_$tag.txt | tail -1 | cut -c1-160)" | tee -a gpurun_out/s32.txt
+  done; done
+  for r in 1 2; do for v in "skip:BDPT_POOL=4" "noskip:BDPT_POOL=4;BDPT_JIT_FLAGS=-DBDPT_POOL_NOSKIP=1"; do
+    tag=${v%%:*}; envs=${v#*:}; IFS=';' read -r -a assign <<< "$envs"
+    env "${assign[@]}" timeout -k 10 200 python scripts/shard_probe.py --scene caustic --passes 128 --strong --reps 30 --ns 8 > gpurun_out/s32_n8_$tag.txt 2>&1 || { tail -5 gpurun_out/s32_n8_$tag.txt; exit 1; }
+    echo "$r N8 $tag $(grep '"streams_req": 0' gpurun_out/s32_n8_$tag.txt | tail -1)" | tee -a gpurun_out/s32.txt
+  done; done
+}
+
+s33() {
+  timeout -k 10 300 python -u -m pytest tests/test_gpu_pool.py tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k "pool or auto" > gpurun_out/s33_pytest.log 2>&1 || { tail -30 gpurun_out/s33_pytest.log; exit 1; }
+  tail -1 gpurun_out/s33_pytest.log
+  for r in 1 2; do for v in "early:" "late:BDPT_JIT_FLAGS=-DBDPT_POOL_EARLY=0"; do
+    tag=${v%%:*}; envs=${v#*:}; IFS=';' read -r -a assign <<< "$envs"
+    env "${assign[@]}" BDPT_POOL=16 timeout -k 10 200 python scripts/probe_step.py --scene caustic --streams 128 --reps 10 --tag $tag > gpurun_out/s33_n1.txt 2>&1 || { tail -5 gpurun_out/s33_n1.txt; exit 1; }
+    echo "$r N1 $(grep '^{' gpurun_out/s33_n1.txt | tail -1 | cut -c1-160)" | tee -a gpurun_out/s33.txt
+    env "${assign[@]}" BDPT_POOL=4 timeout -k 10 200 python scripts/shard_probe.py --scene caustic --passes 128 --strong --reps 30 --ns 8 > gpurun_out/s33_n8.txt 2>&1 || { tail -5 gpurun_out/s33_n8.txt; exit 1; }
+    echo "$r N8 $tag $(grep '"streams_req": 0' gpurun_out/s33_n8.txt | tail -1)" | tee -a gpurun_out/s33.txt
+  done; done
+}
+
 case "${1:-}" in
-  s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29|s30) "$1" ;;
-  *) echo "usage: $0 {s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29|s30}"; exit 2 ;;
+  s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29|s30|s31|s32|s33) "$1" ;;
+  *) echo "usage: $0 {s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29|s30|s31|s32|s33}"; exit 2 ;;
 esac
