@@ -197,7 +197,14 @@ s33() {
   done; done
 }
 
+s34() {
+  for P in 32 64 128; do
+    BDPT_POOL=4 timeout -k 10 200 python scripts/shard_probe.py --scene caustic --passes $P --strong --reps 30 --ns 1,8 > gpurun_out/s34_p$P.txt 2>&1 || { tail -5 gpurun_out/s34_p$P.txt; exit 1; }
+    echo "P=$P $(grep '"streams_req": 0' gpurun_out/s34_p$P.txt | tr '\n' ' ')" | tee -a gpurun_out/s34.txt
+  done
+}
+
 case "${1:-}" in
-  s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29|s30|s31|s32|s33) "$1" ;;
-  *) echo "usage: $0 {s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29|s30|s31|s32|s33}"; exit 2 ;;
+  s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29|s30|s31|s32|s33|s34) "$1" ;;
+  *) echo "usage: $0 {s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29|s30|s31|s32|s33|s34}"; exit 2 ;;
 esac
