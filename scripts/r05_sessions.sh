@@ -204,7 +204,11 @@ s34() {
   done
 }
 
+s35() {
+  ARGS="--scene cornell --streams 64" ROUNDS=2 VARIANTS="k48:BDPT_UNITS=8 k32:BDPT_UNITS=8;BDPT_JIT_FLAGS=-DBDPT_REGEN_K=32 k56:BDPT_UNITS=8;BDPT_JIT_FLAGS=-DBDPT_REGEN_K=56 k64:BDPT_UNITS=8;BDPT_JIT_FLAGS=-DBDPT_REGEN_K=64 k16:BDPT_UNITS=8;BDPT_JIT_FLAGS=-DBDPT_REGEN_K=16" OUT=gpurun_out/s35_regen_units.txt bash scripts/ab.sh || exit 1
+}
+
 case "${1:-}" in
-  s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29|s30|s31|s32|s33|s34) "$1" ;;
-  *) echo "usage: $0 {s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29|s30|s31|s32|s33|s34}"; exit 2 ;;
+  s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29|s30|s31|s32|s33|s34|s35) "$1" ;;
+  *) echo "usage: $0 {s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29|s30|s31|s32|s33|s34|s35}"; exit 2 ;;
 esac
