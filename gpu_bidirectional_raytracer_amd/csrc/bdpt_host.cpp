@@ -62,12 +62,20 @@ struct bdpt_ctx {
     // has read it.  Everything else that touches colors/counter/pixels runs on `stream` after
     // join_fold() has made it wait for the last concurrent fold.
     hipStream_t fstream = nullptr;
+    // Pixel pools with overlapped launches: a pooled launch and its serial fold run on
+    // pstream[half of the radiance buffer], so one launch's drain overlaps the next one's start;
+    // the folds stay in order through rb_fold_ev.  Everything queued on `stream` that feeds or
+    // follows the path kernels joins the last fold first (join_fold).
+    hipStream_t pstream[2] = {nullptr, nullptr};
+    hipEvent_t amark = nullptr;         // `stream`'s work before a call, for the pstreams to wait on
+    bool pool_dirty = false;            // overlapped launches used the claim-counter sets
     unsigned long long* d_prof = nullptr;   // BDPT_PROF=1 (with a -DBDPT_PROF kernel): section cycles
     hipEvent_t rb_path_ev[2] = {nullptr, nullptr};   // path kernel of the half done (stream)
     hipEvent_t rb_fold_ev[2] = {nullptr, nullptr};   // fold of the half done (fstream)
     bool rb_used[2] = {false, false};
     int rb_next = 0, fold_last = 0;
     bool fold_pending = false;          // a fold was issued after the last join_fold
+    hipStream_t fold_stream = nullptr;  // the stream of the last fold (fstream or a pstream)
     // Path-pass calls go through a ring of kRing slots, each with its own events, so a call
     // never waits for the GPU except on the call issued kRing calls earlier (the reference's
     // interactive loop issues one pass per call; the pass tables travel in the kernel
@@ -217,12 +225,15 @@ static int fail(bdpt_ctx* c, int code, const char* fmt, ...) {
             return fail((ctx), BDPT_EHIP, "%s: %s", #call, hipGetErrorString(e_));            \
     } while (0)
 
+static int join_fold(bdpt_ctx* c);
 static int upload_scene(bdpt_ctx* c) {
     c->tune_phase = 0;                                      // re-measure the stream mode
     for (auto& row : c->jit_memo)                           // the specialised kernels change too
         for (auto& m : row) m.valid = false;
     const unsigned n = (unsigned)c->spheres.size();
-    // queued path passes may still read the scene buffers freed / rewritten below
+    // queued path passes may still read the scene buffers freed / rewritten below (pooled
+    // launches on the pstreams: the last fold follows them all)
+    if (int rc = join_fold(c)) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     std::vector<bdpt_dev_sphere> ds(n);
     std::vector<float4> geom(n), lrec;
@@ -329,6 +340,9 @@ static void release(bdpt_ctx* c) {
         if (c->rb_path_ev[b]) (void)hipEventDestroy(c->rb_path_ev[b]);
         if (c->rb_fold_ev[b]) (void)hipEventDestroy(c->rb_fold_ev[b]);
     }
+    if (c->amark) (void)hipEventDestroy(c->amark);
+    for (hipStream_t& ps : c->pstream)
+        if (ps) (void)hipStreamDestroy(ps);
     if (c->fstream) (void)hipStreamDestroy(c->fstream);
     if (c->stream) (void)hipStreamDestroy(c->stream);
 }
@@ -854,6 +868,8 @@ void bdpt_destroy(bdpt_ctx* c) {
     destroy_group(c);
     (void)hipSetDevice(c->device);
     if (c->fstream) (void)hipStreamSynchronize(c->fstream);
+    for (hipStream_t ps : c->pstream)
+        if (ps) (void)hipStreamSynchronize(ps);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->d_prof) {                 // section profile of a -DBDPT_PROF kernel (experiments)
         unsigned long long p[24] = {};
@@ -990,6 +1006,7 @@ static int one_generate_rand(bdpt_ctx* c, unsigned seed) {
         return BDPT_OK;
     }
     HIPCHK(c, hipSetDevice(c->device));
+    if (int rc = join_fold(c)) return rc;              // path kernels read the table
     // seedMTGPU(seed): every record's seed field := seed (MersenneTwister_kernel.cu:44-47)
     std::vector<uint32_t> p(c->h_params, c->h_params + 4 * BDPT_MT_RNG_COUNT);
     for (int i = 0; i < BDPT_MT_RNG_COUNT; i++) p[4 * i + 3] = seed;
@@ -1239,6 +1256,8 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
         if (need > c->rbuf_cap || (size_t)lanes > c->rmask_lanes) {
             HIPCHK(c, hipStreamSynchronize(c->stream));     // queued passes and folds may use it
             HIPCHK(c, hipStreamSynchronize(c->fstream));
+            for (hipStream_t ps : c->pstream)
+                if (ps) HIPCHK(c, hipStreamSynchronize(ps));
             if (c->d_rbuf) HIPCHK(c, hipFree(c->d_rbuf));
             if (c->d_rmask) HIPCHK(c, hipFree(c->d_rmask));
             c->d_rbuf = nullptr;
@@ -1282,12 +1301,28 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
     // path kernel 3.93 -> 3.29-3.31 ms; two passes per lane keep the concurrent fold (cornell
     // S = 64 33.82 -> 33.92 ms serial), profiles/r05_s11_serial_fold.txt.
     const bool serial_fold = jf_pool != nullptr;
+    // Pooled launches overlap: each runs (with its fold) on pstream[half], so a launch's drain --
+    // ~0.1 ms at its end, when all passes' pools run out together and the last paths finish at
+    // falling occupancy -- overlaps the next launch's start (caustic8 +1.1 to +1.7 %, its 1/4 and
+    // 1/8 shares +4 to +6 %, profiles/r05_s37_pool_overlap.txt).  Not in the stream mode's tuning
+    // calls (measured one at a time, as the other modes); BDPT_POOL_OVERLAP=0 turns it off.
+    static const bool overlap_env = !getenv("BDPT_POOL_OVERLAP") || atoi(getenv("BDPT_POOL_OVERLAP")) != 0;
+    const bool overlap = serial_fold && overlap_env && tune_role < 0;
     // a fused launch updates colors itself, and a serial fold does so on this stream: they wait
     // for the outstanding concurrent fold, before the call's timing starts (so the stream-mode
-    // measurement does not charge that fold to it)
-    if (any_fused || jf_units || serial_fold)
+    // measurement does not charge that fold to it); overlapped pooled launches order their folds
+    // through rb_fold_ev instead
+    if (any_fused || jf_units || (serial_fold && !overlap))
         if (int rc = join_fold(c)) return rc;
-    HIPCHK(c, hipEventRecord(cs.ev0, c->stream));
+    if (overlap) {
+        if (!c->pstream[0]) {
+            for (hipStream_t& ps : c->pstream) HIPCHK(c, hipStreamCreateWithFlags(&ps, hipStreamNonBlocking));
+            HIPCHK(c, hipEventCreateWithFlags(&c->amark, hipEventDisableTiming));
+        }
+        HIPCHK(c, hipEventRecord(c->amark, c->stream));  // the pstreams follow `stream`'s earlier work
+    }
+    bool ev0_done = !overlap;
+    if (!overlap) HIPCHK(c, hipEventRecord(cs.ev0, c->stream));
     int launches = 0;
     for (int p0 = 0; grid_rows > 0 && p0 < npass; p0 += chunk, launches++) {
         a.npass = npass - p0 < chunk ? npass - p0 : chunk;
@@ -1329,6 +1364,17 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
         void* kargs[] = {&a};
         grid.z = a.streams;
         const int half = c->rb_next;
+        // the stream of this launch (and of its fold): `stream`, or pstream[half] for an
+        // overlapped pooled launch
+        hipStream_t ls = c->stream;
+        if (pooled && overlap) {
+            ls = c->pstream[half];
+            HIPCHK(c, hipStreamWaitEvent(ls, c->amark, 0));
+        }
+        if (!ev0_done) {                                     // the call's time starts here
+            HIPCHK(c, hipEventRecord(cs.ev0, ls));
+            ev0_done = true;
+        }
         if (unitsl) {
             // the units fold in the kernel: no radiance buffer; the previous call's folds were
             // joined above
@@ -1336,12 +1382,12 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
             a.rmask = nullptr;
         } else if (st) {
             // this half was last read by the fold of the launch before the previous one
-            if (c->rb_used[half]) HIPCHK(c, hipStreamWaitEvent(c->stream, c->rb_fold_ev[half], 0));
+            if (c->rb_used[half]) HIPCHK(c, hipStreamWaitEvent(ls, c->rb_fold_ev[half], 0));
             a.rbuf = c->d_rbuf + (size_t)half * c->rbuf_cap;
             a.rmask = c->d_rmask + (size_t)half * 4 * c->rmask_lanes;
             // pools mark their stored samples in the mask: cleared first (the fold that read this
             // half ran earlier on this stream)
-            if (jf_pool) HIPCHK(c, hipMemsetAsync(a.rmask, 0, 16 * (size_t)lanes, c->stream));
+            if (jf_pool) HIPCHK(c, hipMemsetAsync(a.rmask, 0, 16 * (size_t)lanes, ls));
         } else if (int rc = join_fold(c)) {                  // the fused kernel updates colors itself
             return rc;
         }
@@ -1362,9 +1408,22 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
             int R = 1, G = 1;
             pool_shape(lanes, &R, &G);
             a.pool = R;
-            a.pool_ctr = c->d_poolctr + (size_t)c->pool_set * kSet;
-            a.pool_ctr_next = c->d_poolctr + (size_t)(c->pool_set ^ 1) * kSet;
-            c->pool_set ^= 1;
+            if (overlap) {
+                // set `half`, cleared on this launch's stream (its previous user, the launch two
+                // back, ran earlier on the same stream); the kernel clears no next set
+                a.pool_ctr = c->d_poolctr + (size_t)half * kSet;
+                a.pool_ctr_next = nullptr;
+                HIPCHK(c, hipMemsetAsync(a.pool_ctr, 0, kSet * sizeof(unsigned), ls));
+                c->pool_dirty = true;
+            } else {
+                if (c->pool_dirty) {                         // overlapped launches left both sets used
+                    HIPCHK(c, hipMemsetAsync(c->d_poolctr, 0, 2 * kSet * sizeof(unsigned), c->stream));
+                    c->pool_dirty = false;
+                }
+                a.pool_ctr = c->d_poolctr + (size_t)c->pool_set * kSet;
+                a.pool_ctr_next = c->d_poolctr + (size_t)(c->pool_set ^ 1) * kSet;
+                c->pool_set ^= 1;
+            }
             // 1-D, passes interleaved in groups of 8 workgroups (bdpt_kernels.hip s0)
             const long span = 256L * G, per = ((lanes + span - 1) / span + 7) / 8 * 8;
             pgrid = dim3((unsigned)(per * a.streams), 1, 1);
@@ -1403,19 +1462,33 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
             c->units_check = true;
             units_ran = true;
         }
-        HIPCHK(c, hipEventRecord(cs.kev[2 * launches], c->stream));
+        HIPCHK(c, hipEventRecord(cs.kev[2 * launches], ls));
         if (jf)
             HIPCHK(c, hipModuleLaunchKernel(jf, pgrid.x, pgrid.y, pgrid.z, block.x, 1, 1, (unsigned)smem,
-                                            c->stream, kargs, nullptr));
+                                            ls, kargs, nullptr));
         else
-            HIPCHK(c, hipLaunchKernel(kern, grid, block, kargs, smem, c->stream));
-        HIPCHK(c, hipEventRecord(cs.kev[2 * launches + 1], c->stream));
+            HIPCHK(c, hipLaunchKernel(kern, grid, block, kargs, smem, ls));
+        HIPCHK(c, hipEventRecord(cs.kev[2 * launches + 1], ls));
         const dim3 fgrid((unsigned)((lanes + 255) / 256), 1, 1);   // the fold: 1-D over the launch's rows
         if (st && !unitsl && serial_fold) {                 // the fold after the path kernel
-            HIPCHK(c, hipLaunchKernel((const void*)&bdpt_accum_serial_kernel, fgrid, block, kargs, 0, c->stream));
+            // (overlapped: after the previous fold too, wherever it ran)
+            if (overlap && c->fold_pending) HIPCHK(c, hipStreamWaitEvent(ls, c->rb_fold_ev[c->fold_last], 0));
+            HIPCHK(c, hipLaunchKernel((const void*)&bdpt_accum_serial_kernel, fgrid, block, kargs, 0, ls));
+            if (overlap) {
+                HIPCHK(c, hipEventRecord(c->rb_fold_ev[half], ls));
+                c->rb_used[half] = true;
+                c->fold_last = half;
+                c->fold_pending = true;
+                c->fold_stream = ls;
+                c->rb_next = half ^ 1;
+            }
         } else if (st && !unitsl) {                         // the ordered fold, on fstream
             HIPCHK(c, hipEventRecord(c->rb_path_ev[half], c->stream));
             HIPCHK(c, hipStreamWaitEvent(c->fstream, c->rb_path_ev[half], 0));
+            // after the previous fold (an overlapped pooled launch's ran on a pstream)
+            if (c->fold_pending && c->fold_stream != c->fstream)
+                HIPCHK(c, hipStreamWaitEvent(c->fstream, c->rb_fold_ev[c->fold_last], 0));
+            c->fold_stream = c->fstream;
             HIPCHK(c, hipLaunchKernel((const void*)&bdpt_accum_kernel, fgrid, block, kargs, 0, c->fstream));
             HIPCHK(c, hipEventRecord(c->rb_fold_ev[half], c->fstream));
             c->rb_used[half] = true;
@@ -1426,7 +1499,7 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
     }
     // the call ends with its last fold (fstream, which waited for the path kernels) if one is
     // outstanding, else on the context's stream
-    HIPCHK(c, hipEventRecord(cs.ev1, c->fold_pending ? c->fstream : c->stream));
+    HIPCHK(c, hipEventRecord(cs.ev1, c->fold_pending ? c->fold_stream : c->stream));
     cs.launches = launches;
     cs.pending = true;
     cs.serial_fold = serial_fold;

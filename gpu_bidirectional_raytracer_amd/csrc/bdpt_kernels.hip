@@ -705,9 +705,11 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
     __shared__ unsigned pool_left;
     if constexpr (kPool) {
         // the next pooled launch's counters (the previous launch used them and has finished);
-        // before the early exit, so every workgroup does its share
-        for (unsigned w = blockIdx.x * 256u + threadIdx.x; w < 128u * 8u; w += gridDim.x * 256u)
-            a.pool_ctr_next[w * 32u] = 0u;
+        // before the early exit, so every workgroup does its share.  (Overlapped launches: none,
+        // the host clears each launch's set on its stream.)
+        if (a.pool_ctr_next)
+            for (unsigned w = blockIdx.x * 256u + threadIdx.x; w < 128u * 8u; w += gridDim.x * 256u)
+                a.pool_ctr_next[w * 32u] = 0u;
     }
     if (kPool && threadIdx.x == 0) pool_left = 0u;
     __syncthreads();

@@ -208,7 +208,36 @@ s35() {
   ARGS="--scene cornell --streams 64" ROUNDS=2 VARIANTS="k48:BDPT_UNITS=8 k32:BDPT_UNITS=8;BDPT_JIT_FLAGS=-DBDPT_REGEN_K=32 k56:BDPT_UNITS=8;BDPT_JIT_FLAGS=-DBDPT_REGEN_K=56 k64:BDPT_UNITS=8;BDPT_JIT_FLAGS=-DBDPT_REGEN_K=64 k16:BDPT_UNITS=8;BDPT_JIT_FLAGS=-DBDPT_REGEN_K=16" OUT=gpurun_out/s35_regen_units.txt bash scripts/ab.sh || exit 1
 }
 
+s36() {
+  BDPT_POOL_OVERLAP=1 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "pool or auto or stream or fold or caustic or shard or config or multi or checkpoint or replay" > gpurun_out/s36_pytest_overlap.log 2>&1 || { tail -30 gpurun_out/s36_pytest_overlap.log; exit 1; }
+  tail -1 gpurun_out/s36_pytest_overlap.log
+  timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "pool or auto" > gpurun_out/s36_pytest.log 2>&1 || { tail -30 gpurun_out/s36_pytest.log; exit 1; }
+  tail -1 gpurun_out/s36_pytest.log
+  MODE=bench ARGS="--workload caustic8 --no-cpu-baseline --steps 20" ROUNDS=2 VARIANTS="serial: overlap:BDPT_POOL_OVERLAP=1" OUT=gpurun_out/s36_ab.txt bash scripts/ab.sh || exit 1
+  for r in 1 2; do for v in "serial:BDPT_POOL=4" "overlap:BDPT_POOL=4;BDPT_POOL_OVERLAP=1"; do
+    tag=${v%%:*}; envs=${v#*:}; IFS=';' read -r -a assign <<< "$envs"
+    env "${assign[@]}" timeout -k 10 200 python scripts/shard_probe.py --scene caustic --passes 128 --strong --reps 30 --ns 8 > gpurun_out/s36_n8.txt 2>&1 || { tail -5 gpurun_out/s36_n8.txt; exit 1; }
+    echo "$r N8 $tag $(grep '"streams_req": 0' gpurun_out/s36_n8.txt | tail -1)" | tee -a gpurun_out/s36_ab.txt
+  done; done
+}
+
+s37() {
+  BDPT_POOL_OVERLAP=1 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "pool or auto or caustic or multi or checkpoint" > gpurun_out/s37_pytest_overlap.log 2>&1 || { tail -30 gpurun_out/s37_pytest_overlap.log; exit 1; }
+  tail -1 gpurun_out/s37_pytest_overlap.log
+  MODE=bench ARGS="--workload caustic8 --no-cpu-baseline --steps 20" ROUNDS=2 VARIANTS="serial: overlap:BDPT_POOL_OVERLAP=1" OUT=gpurun_out/s37_ab.txt bash scripts/ab.sh || exit 1
+  for r in 1 2; do for v in "serial:BDPT_POOL=16" "overlap:BDPT_POOL=16;BDPT_POOL_OVERLAP=1"; do
+    tag=${v%%:*}; envs=${v#*:}; IFS=';' read -r -a assign <<< "$envs"
+    env "${assign[@]}" timeout -k 10 200 python scripts/probe_step.py --scene caustic --streams 128 --reps 20 --tag $tag > gpurun_out/s37_n1.txt 2>&1 || { tail -5 gpurun_out/s37_n1.txt; exit 1; }
+    echo "$r N1 $(grep '^{' gpurun_out/s37_n1.txt | tail -1 | cut -c1-140)" | tee -a gpurun_out/s37_ab.txt
+  done; done
+  for r in 1 2; do for v in "serial:" "overlap:BDPT_POOL_OVERLAP=1"; do
+    tag=${v%%:*}; envs=${v#*:}; IFS=';' read -r -a assign <<< "$envs"
+    env "${assign[@]}" timeout -k 10 300 python scripts/shard_probe.py --scene caustic --passes 128 --strong --reps 30 > gpurun_out/s37_strong.txt 2>&1 || { tail -5 gpurun_out/s37_strong.txt; exit 1; }
+    echo "$r strong $tag $(grep '"streams_req": 0' gpurun_out/s37_strong.txt | cut -c1-120 | tr '\n' ' ')" | tee -a gpurun_out/s37_ab.txt
+  done; done
+}
+
 case "${1:-}" in
-  s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29|s30|s31|s32|s33|s34|s35) "$1" ;;
-  *) echo "usage: $0 {s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29|s30|s31|s32|s33|s34|s35}"; exit 2 ;;
+  s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29|s30|s31|s32|s33|s34|s35|s36|s37) "$1" ;;
+  *) echo "usage: $0 {s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29|s30|s31|s32|s33|s34|s35|s36|s37}"; exit 2 ;;
 esac
