@@ -237,7 +237,16 @@ s37() {
   done; done
 }
 
+s38() {
+  for v in "overlap:" "serial:BDPT_POOL_OVERLAP=0"; do
+    tag=${v%%:*}; envs=${v#*:}; IFS=';' read -r -a assign <<< "$envs"
+    rm -rf gpurun_out/prof_s38_$tag
+    env "${assign[@]}" timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_s38_$tag -o run --output-format csv -- python3 bench.py --workload caustic8 --no-cpu-baseline --steps 20 > gpurun_out/prof_s38_$tag.log 2>&1 || exit 1
+    echo "$tag $(grep '^{' gpurun_out/prof_s38_$tag.log | tail -1 | cut -c1-100)"; head -3 gpurun_out/prof_s38_$tag/run_kernel_stats.csv | cut -c1-120
+  done
+}
+
 case "${1:-}" in
-  s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29|s30|s31|s32|s33|s34|s35|s36|s37) "$1" ;;
-  *) echo "usage: $0 {s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29|s30|s31|s32|s33|s34|s35|s36|s37}"; exit 2 ;;
+  s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29|s30|s31|s32|s33|s34|s35|s36|s37|s38) "$1" ;;
+  *) echo "usage: $0 {s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29|s30|s31|s32|s33|s34|s35|s36|s37|s38}"; exit 2 ;;
 esac
