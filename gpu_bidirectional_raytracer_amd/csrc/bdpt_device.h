@@ -112,7 +112,43 @@ struct bdpt_path_args {
     unsigned* unit_flags;           // per 8x8 wave tile: epoch << 8 | ranges folded
     unsigned* unit_err;             // non-zero: a handover wait timed out (ordering violated)
     unsigned* unit_ctr;             // per XCD queue: units claimed (8 counters, 128 B apart, zeroed per launch)
+    int unit_taper;                 // 1: the launch's last unit_passes passes in halving ranges
 };
+
+// Units' pass ranges: unit_passes (P) passes each, except (taper) the launch's last <= P passes,
+// which are split in halves -- P = 8: ..., 8, 4, 2, 1, 1 -- so that the launch drains over short
+// units (the tiles' last ranges are what runs while the chip empties).  Range r starts at the
+// returned pass and holds *len passes; bdpt_unit_ranges counts them.
+__host__ __device__ inline int bdpt_unit_range(int npass, int P, int taper, int r, int* len) {
+    if (!taper) {
+        const int s = r * P;
+        *len = npass - s < P ? npass - s : P;
+        return s;
+    }
+    const int nbig = (npass - 1) / P;
+    if (r < nbig) {
+        *len = P;
+        return r * P;
+    }
+    int s = nbig * P, T = npass - s;
+    for (int t = r - nbig; t > 0; t--) {
+        const int h = (T + 1) / 2;
+        s += h;
+        T -= h;
+    }
+    *len = T > 1 ? (T + 1) / 2 : T;
+    return s;
+}
+__host__ __device__ inline int bdpt_unit_ranges(int npass, int P, int taper) {
+    if (!taper) return (npass + P - 1) / P;
+    const int nbig = (npass - 1) / P;
+    int T = npass - nbig * P, n = nbig;
+    while (T > 0) {
+        T -= T > 1 ? (T + 1) / 2 : 1;
+        n++;
+    }
+    return n;
+}
 
 // Tile row of a workgroup row: identity, or the sub-th tile row of this shard's k-th band.
 __device__ __forceinline__ int bdpt_dev_tile_row(const bdpt_path_args& a, int by) {

@@ -1432,7 +1432,10 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
         if (unitsl) {
             // one workgroup per unit; each claims its unit from its XCD's queue (bdpt_kernels.hip)
             const int wgs = (int)grid.x * grid_rows;
-            const int nranges = (a.npass + a.unit_passes - 1) / a.unit_passes;
+            // the last passes in halving ranges (bdpt_device.h bdpt_unit_range); BDPT_UNITS_TAPER=0 off
+            static const int taper = getenv("BDPT_UNITS_TAPER") ? atoi(getenv("BDPT_UNITS_TAPER")) != 0 : 1;
+            a.unit_taper = taper;
+            const int nranges = bdpt_unit_ranges(a.npass, a.unit_passes, a.unit_taper);
             const size_t nflags = (size_t)wgs * 4;
             if (!c->d_uerr) {                                // error word + 8 queue counters, 128 B apart
                 HIPCHK(c, hipMalloc(&c->d_uerr, sizeof(unsigned) * (32 + 8 * 32)));

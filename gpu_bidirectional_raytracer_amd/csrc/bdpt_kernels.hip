@@ -625,7 +625,7 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
     if constexpr (kUnits) {
         __shared__ unsigned uclaim[2];
         if (threadIdx.x == 0) {
-            const unsigned wgs = (unsigned)a.unit_wgs, nr = (unsigned)((a.npass + a.unit_passes - 1) / a.unit_passes);
+            const unsigned wgs = (unsigned)a.unit_wgs, nr = (unsigned)bdpt_unit_ranges(a.npass, a.unit_passes, a.unit_taper);
             const unsigned xcd = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 7u;   // XCC_ID
             uclaim[0] = 0xffffffffu;
             for (unsigned k = 0; k < 8u; k++) {
@@ -649,10 +649,10 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
     const int vbx = kUnits ? vtile % a.gx : (int)blockIdx.x, vby = kUnits ? vtile / a.gx : (int)blockIdx.y;
     const int vgx = kUnits ? a.gx : (int)gridDim.x, vgy = kUnits ? a.gy : (int)gridDim.y;
     const int S = kUnits ? 1 : (STREAMS ? a.streams : 1);
-    const int s0 = kUnits ? (int)urange * a.unit_passes
+    int ulen = 0;
+    const int s0 = kUnits ? bdpt_unit_range(a.npass, a.unit_passes, a.unit_taper, (int)urange, &ulen)
                  : !STREAMS ? 0 : kPool ? (int)((blockIdx.x >> 3) % (unsigned)S) : (int)blockIdx.z;
-    const int nslot = kUnits ? (a.npass - s0 < a.unit_passes ? a.npass - s0 : a.unit_passes)
-                             : (a.npass - s0 + S - 1) / S;
+    const int nslot = kUnits ? ulen : (a.npass - s0 + S - 1) / S;
     const int mslot = kUnits ? a.unit_passes : (a.npass + S - 1) / S;   // slots of the LDS layout (any s0)
     float4* C = smem;                 // {cx, cy, cz, bits(refl | emissive<<8)}
     float4* E = smem + n;             // {ex, ey, ez, rad}

@@ -246,7 +246,22 @@ s38() {
   done
 }
 
+s39() {
+  for P in 32 64 128; do
+    BDPT_UNITS=8 timeout -k 10 200 python scripts/probe_step.py --scene cornell --passes $P --streams 64 --reps 4 --tag u$P > gpurun_out/s39_u$P.txt 2>&1 || { tail -5 gpurun_out/s39_u$P.txt; exit 1; }
+    echo "units P=$P $(grep '^{' gpurun_out/s39_u$P.txt | tail -1 | cut -c1-170)" | tee -a gpurun_out/s39.txt
+    timeout -k 10 200 python scripts/probe_step.py --scene cornell --passes $P --streams $((P/2)) --reps 4 --tag s$P > gpurun_out/s39_s$P.txt 2>&1 || { tail -5 gpurun_out/s39_s$P.txt; exit 1; }
+    echo "streams P=$P $(grep '^{' gpurun_out/s39_s$P.txt | tail -1 | cut -c1-170)" | tee -a gpurun_out/s39.txt
+  done
+}
+
+s40() {
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_units.py tests/test_gpu_parity.py tests/test_gpu_configs.py -x -q --timeout 300 --timeout-method thread > gpurun_out/s40_pytest.log 2>&1 || { tail -30 gpurun_out/s40_pytest.log; exit 1; }
+  tail -1 gpurun_out/s40_pytest.log
+  ARGS="--scene cornell --streams 64" ROUNDS=3 VARIANTS="taper:BDPT_UNITS=8 flat:BDPT_UNITS=8;BDPT_UNITS_TAPER=0 s64:" OUT=gpurun_out/s40_ab.txt bash scripts/ab.sh || exit 1
+}
+
 case "${1:-}" in
-  s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29|s30|s31|s32|s33|s34|s35|s36|s37|s38) "$1" ;;
-  *) echo "usage: $0 {s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29|s30|s31|s32|s33|s34|s35|s36|s37|s38}"; exit 2 ;;
+  s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29|s30|s31|s32|s33|s34|s35|s36|s37|s38|s39|s40) "$1" ;;
+  *) echo "usage: $0 {s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29|s30|s31|s32|s33|s34|s35|s36|s37|s38|s39|s40}"; exit 2 ;;
 esac
