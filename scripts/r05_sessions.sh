@@ -261,7 +261,14 @@ s40() {
   ARGS="--scene cornell --streams 64" ROUNDS=3 VARIANTS="taper:BDPT_UNITS=8 flat:BDPT_UNITS=8;BDPT_UNITS_TAPER=0 s64:" OUT=gpurun_out/s40_ab.txt bash scripts/ab.sh || exit 1
 }
 
+s41() {
+  for U in 4 8 16; do for P in 32 128; do
+    BDPT_UNITS=$U timeout -k 10 200 python scripts/probe_step.py --scene cornell --passes $P --streams 64 --reps 4 --tag u${U}p$P > gpurun_out/s41.tmp 2>&1 || { tail -5 gpurun_out/s41.tmp; exit 1; }
+    echo "U=$U P=$P $(grep '^{' gpurun_out/s41.tmp | tail -1 | cut -c1-150)" | tee -a gpurun_out/s41.txt
+  done; done
+}
+
 case "${1:-}" in
-  s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29|s30|s31|s32|s33|s34|s35|s36|s37|s38|s39|s40) "$1" ;;
-  *) echo "usage: $0 {s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29|s30|s31|s32|s33|s34|s35|s36|s37|s38|s39|s40}"; exit 2 ;;
+  s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29|s30|s31|s32|s33|s34|s35|s36|s37|s38|s39|s40|s41) "$1" ;;
+  *) echo "usage: $0 {s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29|s30|s31|s32|s33|s34|s35|s36|s37|s38|s39|s40|s41}"; exit 2 ;;
 esac
