@@ -158,3 +158,14 @@ def test_valu_attribution_anchors():
     src = open(va.SRC).read()
     sites = {int(m.group(1)) for m in re.finditer(r"BDPT_CNTN?\((\d+),", src)}
     assert sites >= set(range(16)) - {va.C_REFR}, sorted(sites)
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="no hipcc")
+def test_unit_ranges_partition(tmp_path):
+    """The units' pass ranges (bdpt_device.h, shared by kernel and launcher) partition every
+    launch in order, with the halving tail (tests/native/unit_ranges_check.cpp)."""
+    exe = tmp_path / "unit_ranges_check"
+    subprocess.check_call([HIPCC, "-O1", "-std=c++17", "-o", str(exe),
+                           os.path.join(REPO, "tests", "native", "unit_ranges_check.cpp")])
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
+    assert out.returncode == 0 and out.stdout.startswith("ok"), out.stdout
