@@ -268,7 +268,16 @@ s41() {
   done; done
 }
 
+s42() {
+  for v in "table:" "ablate:BDPT_JIT_FLAGS=-DBDPT_SCT_ABLATE=1"; do
+    tag=${v%%:*}; envs=${v#*:}; IFS=';' read -r -a assign <<< "$envs"
+    rm -rf gpurun_out/pmc_s42_$tag
+    env "${assign[@]}" BDPT_UNITS=8 timeout -s KILL 240 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE --kernel-trace -d gpurun_out/pmc_s42_$tag -o run --output-format csv -- python3 scripts/probe_step.py --scene cornell --streams 64 --reps 2 --tag $tag > gpurun_out/pmc_s42_$tag.log 2>&1 || exit 1
+    echo "$tag done"
+  done
+}
+
 case "${1:-}" in
-  s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29|s30|s31|s32|s33|s34|s35|s36|s37|s38|s39|s40|s41) "$1" ;;
-  *) echo "usage: $0 {s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29|s30|s31|s32|s33|s34|s35|s36|s37|s38|s39|s40|s41}"; exit 2 ;;
+  s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29|s30|s31|s32|s33|s34|s35|s36|s37|s38|s39|s40|s41|s42) "$1" ;;
+  *) echo "usage: $0 {s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29|s30|s31|s32|s33|s34|s35|s36|s37|s38|s39|s40|s41|s42}"; exit 2 ;;
 esac
