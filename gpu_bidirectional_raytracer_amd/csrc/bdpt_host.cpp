@@ -565,20 +565,23 @@ static int pool_env() {
     const int v = atoi(e);
     return v < 1 ? 0 : (v > 64 ? 64 : v);
 }
-// Launch shape of a pooled launch of nloc pixels per pass: {chunk R, grid G}.  One-session probe
-// (profiles/r04_s18_*): caustic 1921 x 1081 best at G = 64, R = 16 on the whole frame; its
-// 1/8 band (260 K pixels) best at G = 16..32, R = 2..4 (fewer waves per pass fill the chip only
-// with smaller G; chunks of G/4 keep ~4 claims per wave); with the sparse serial fold, three
-// interleaved rounds put G = 16 3 % ahead of G = 32 there (profiles/r05_s20_pool_grid_n8.txt).
+// Launch shape of a pooled launch of nloc pixels per pass: {chunk R, grid G} (a wave claims R x 64
+// pixels at a time; a pass has nloc / (256 G) workgroups).  With the sparse serial fold and
+// overlapped launches, larger chunks and grids measured best, except on the 1/8 share
+// (profiles/r05_s44_pool_shape.txt, r05_s45_*, r05_s46_*; two interleaved rounds each, ms per
+// step): whole frame (2.08 M) G = 128, R = 64 3.54-3.55 against G = 64, R = 16 3.66-3.68;
+// 1/2 share G = 128, R = 32 1.88-1.89 against 1.95-1.96; 1/4 share 0.943-0.954 against
+// 0.956-0.962; 1/8 share (260 K) G = 64, R = 16 0.525-0.535 (G = 128: 0.533-0.602).
 static void pool_shape(long nloc, int* R, int* G) {
-    int g = nloc >= (1L << 20) ? 64 : (nloc >= (1L << 19) ? 32 : 16);
+    int g = nloc >= 400000 ? 128 : 64;
+    int r = nloc >= 1500000 ? 64 : (nloc >= 400000 ? 32 : 16);
     if (const char* e = getenv("BDPT_POOL_GRID")) {
         const int v = atoi(e);
         if (v >= 1) g = v > 256 ? 256 : v;
     }
     const int pe = pool_env();
     *G = g;
-    *R = pe > 0 ? pe : (g / 4 < 1 ? 1 : g / 4);
+    *R = pe > 0 ? pe : r;
 }
 
 // The specialised kernel for the context's scene and pass-stream mode, compiled on first use;

@@ -277,7 +277,28 @@ s42() {
   done
 }
 
+s44() {
+  ARGS="--scene caustic --streams 128 --reps 10" ROUNDS=2 VARIANTS="g64r16:BDPT_POOL=16;BDPT_POOL_GRID=64 g32r8:BDPT_POOL=8;BDPT_POOL_GRID=32 g128r32:BDPT_POOL=32;BDPT_POOL_GRID=128 g64r8:BDPT_POOL=8;BDPT_POOL_GRID=64 g64r32:BDPT_POOL=32;BDPT_POOL_GRID=64" OUT=gpurun_out/s44_pool_shape.txt bash scripts/ab.sh || exit 1
+}
+
+s45() {
+  ARGS="--scene caustic --streams 128 --reps 10" ROUNDS=2 VARIANTS="g128r32:BDPT_POOL=32;BDPT_POOL_GRID=128 g256r64:BDPT_POOL=64;BDPT_POOL_GRID=256 g128r64:BDPT_POOL=64;BDPT_POOL_GRID=128 g256r32:BDPT_POOL=32;BDPT_POOL_GRID=256" OUT=gpurun_out/s45_pool_shape.txt bash scripts/ab.sh || exit 1
+  for r in 1 2; do for v in "g16r4:BDPT_POOL=4;BDPT_POOL_GRID=16" "g32r8:BDPT_POOL=8;BDPT_POOL_GRID=32" "g64r16:BDPT_POOL=16;BDPT_POOL_GRID=64"; do
+    tag=${v%%:*}; envs=${v#*:}; IFS=';' read -r -a assign <<< "$envs"
+    env "${assign[@]}" timeout -k 10 300 python scripts/shard_probe.py --scene caustic --passes 128 --strong --reps 30 --ns 4,8 > gpurun_out/s45_sh.txt 2>&1 || { tail -5 gpurun_out/s45_sh.txt; exit 1; }
+    echo "$r $tag $(grep '"streams_req": 0' gpurun_out/s45_sh.txt | cut -c1-75 | tr '\n' ' ')" | tee -a gpurun_out/s45_pool_shape.txt
+  done; done
+}
+
+s46() {
+  for r in 1 2; do for v in "g64r16:BDPT_POOL=16;BDPT_POOL_GRID=64" "g128r32:BDPT_POOL=32;BDPT_POOL_GRID=128" "g128r64:BDPT_POOL=64;BDPT_POOL_GRID=128" "g64r32:BDPT_POOL=32;BDPT_POOL_GRID=64"; do
+    tag=${v%%:*}; envs=${v#*:}; IFS=';' read -r -a assign <<< "$envs"
+    env "${assign[@]}" timeout -k 10 300 python scripts/shard_probe.py --scene caustic --passes 128 --strong --reps 30 --ns 2,4,8 > gpurun_out/s46_sh.txt 2>&1 || { tail -5 gpurun_out/s46_sh.txt; exit 1; }
+    echo "$r $tag $(grep '"streams_req": 0' gpurun_out/s46_sh.txt | cut -c1-75 | tr '\n' ' ')" | tee -a gpurun_out/s46_pool_shape.txt
+  done; done
+}
+
 case "${1:-}" in
-  s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29|s30|s31|s32|s33|s34|s35|s36|s37|s38|s39|s40|s41|s42) "$1" ;;
-  *) echo "usage: $0 {s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29|s30|s31|s32|s33|s34|s35|s36|s37|s38|s39|s40|s41|s42}"; exit 2 ;;
+  s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29|s30|s31|s32|s33|s34|s35|s36|s37|s38|s39|s40|s41|s42|s44|s45|s46) "$1" ;;
+  *) echo "usage: $0 {s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29|s30|s31|s32|s33|s34|s35|s36|s37|s38|s39|s40|s41|s42|s44|s45|s46}"; exit 2 ;;
 esac
