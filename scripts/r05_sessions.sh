@@ -298,7 +298,16 @@ s46() {
   done; done
 }
 
+s47() {
+  timeout -k 10 300 python -u -m pytest tests/test_gpu_pool.py tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k "pool or auto" > gpurun_out/s47_pytest.log 2>&1 || { tail -30 gpurun_out/s47_pytest.log; exit 1; }
+  tail -1 gpurun_out/s47_pytest.log
+  timeout -k 10 300 python bench.py --workload caustic8 > gpurun_out/s47_bench_caustic8.json 2> gpurun_out/s47_bench_caustic8.err || exit 1
+  tail -1 gpurun_out/s47_bench_caustic8.json | cut -c1-120
+  timeout -k 10 500 python scripts/shard_probe.py --scene caustic --passes 128 --strong --reps 30 > gpurun_out/s47_strong.txt 2>&1 || { tail -5 gpurun_out/s47_strong.txt; exit 1; }
+  grep '"streams_req": 0' gpurun_out/s47_strong.txt | cut -c1-150
+}
+
 case "${1:-}" in
-  s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29|s30|s31|s32|s33|s34|s35|s36|s37|s38|s39|s40|s41|s42|s44|s45|s46) "$1" ;;
-  *) echo "usage: $0 {s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29|s30|s31|s32|s33|s34|s35|s36|s37|s38|s39|s40|s41|s42|s44|s45|s46}"; exit 2 ;;
+  s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29|s30|s31|s32|s33|s34|s35|s36|s37|s38|s39|s40|s41|s42|s44|s45|s46|s47) "$1" ;;
+  *) echo "usage: $0 {s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29|s30|s31|s32|s33|s34|s35|s36|s37|s38|s39|s40|s41|s42|s44|s45|s46|s47}"; exit 2 ;;
 esac
