@@ -567,14 +567,18 @@ static int pool_env() {
 }
 // Launch shape of a pooled launch of nloc pixels per pass: {chunk R, grid G} (a wave claims R x 64
 // pixels at a time; a pass has nloc / (256 G) workgroups).  With the sparse serial fold and
-// overlapped launches, larger chunks and grids measured best, except on the 1/8 share
-// (profiles/r05_s44_pool_shape.txt, r05_s45_*, r05_s46_*; two interleaved rounds each, ms per
-// step): whole frame (2.08 M) G = 128, R = 64 3.54-3.55 against G = 64, R = 16 3.66-3.68;
-// 1/2 share G = 128, R = 32 1.88-1.89 against 1.95-1.96; 1/4 share 0.943-0.954 against
-// 0.956-0.962; 1/8 share (260 K) G = 64, R = 16 0.525-0.535 (G = 128: 0.533-0.602).
-static void pool_shape(long nloc, int* R, int* G) {
-    int g = nloc >= 400000 ? 128 : 64;
-    int r = nloc >= 1500000 ? 64 : (nloc >= 400000 ? 32 : 16);
+// overlapped launches, larger chunks and grids measured best (profiles/r05_s44_pool_shape.txt,
+// r05_s45_*, r05_s46_*, r05_s48_*, r05_s49_*; interleaved rounds, ms per step): whole frame
+// (2.08 M) G = 128, R = 64 3.54-3.55 against G = 64, R = 16 3.66-3.68; 1/2 share G = 128, R = 32
+// 1.88-1.89 against 1.95-1.96; 1/4 share 0.943-0.954 against 0.956-0.962; 1/8 share (260 K)
+// G = 128, R = 16 0.548-0.553 against G = 64, R = 16 0.567-0.568 and G = 128, R = 32 0.576-0.578.
+// Launches that are not overlapped (the auto-tuner's calls, BDPT_POOL_OVERLAP=0) keep the shape
+// that measured best before the overlap, G = 64, R = 16: a serial launch pays the large shapes'
+// drain in full, and with them the tuner's pooled call at the 1/8 share lost to S = 32
+// (r05_s50_strong.txt, N = 8 row).
+static void pool_shape(long nloc, bool overlap, int* R, int* G) {
+    int g = overlap ? 128 : 64;
+    int r = !overlap ? 16 : nloc >= 1500000 ? 64 : (nloc >= 400000 ? 32 : 16);
     if (const char* e = getenv("BDPT_POOL_GRID")) {
         const int v = atoi(e);
         if (v >= 1) g = v > 256 ? 256 : v;
@@ -1409,7 +1413,7 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
                 c->pool_set = 0;
             }
             int R = 1, G = 1;
-            pool_shape(lanes, &R, &G);
+            pool_shape(lanes, overlap, &R, &G);
             a.pool = R;
             if (overlap) {
                 // set `half`, cleared on this launch's stream (its previous user, the launch two

@@ -315,7 +315,36 @@ s48() {
   done; done
 }
 
+s49() {
+  for r in 1 2 3; do for v in "g64r16:BDPT_POOL=16;BDPT_POOL_GRID=64" "g128r16:BDPT_POOL=16;BDPT_POOL_GRID=128" "g128r32:BDPT_POOL=32;BDPT_POOL_GRID=128" "g256r16:BDPT_POOL=16;BDPT_POOL_GRID=256" "g128r8:BDPT_POOL=8;BDPT_POOL_GRID=128" "g256r8:BDPT_POOL=8;BDPT_POOL_GRID=256"; do
+    tag=${v%%:*}; envs=${v#*:}; IFS=';' read -r -a assign <<< "$envs"
+    env "${assign[@]}" timeout -k 10 300 python scripts/shard_probe.py --scene caustic --passes 128 --strong --reps 30 --ns 8 > gpurun_out/s49_sh.txt 2>&1 || { tail -5 gpurun_out/s49_sh.txt; exit 1; }
+    echo "$r $tag $(grep '"streams_req": 0' gpurun_out/s49_sh.txt | cut -c1-75 | tr '\n' ' ')" | tee -a gpurun_out/s49_pool_shape_eighth.txt
+  done; done
+}
+
+s50() {
+  timeout -k 10 300 python -u -m pytest tests/test_gpu_pool.py -x -q --timeout 300 --timeout-method thread > gpurun_out/s50_pytest.log 2>&1 || { tail -30 gpurun_out/s50_pytest.log; exit 1; }
+  tail -1 gpurun_out/s50_pytest.log
+  for r in 1 2; do for v in "g128r32:BDPT_POOL=32;BDPT_POOL_GRID=128" "g128r16:BDPT_POOL=16;BDPT_POOL_GRID=128"; do
+    tag=${v%%:*}; envs=${v#*:}; IFS=';' read -r -a assign <<< "$envs"
+    env "${assign[@]}" timeout -k 10 300 python scripts/shard_probe.py --scene caustic --passes 128 --strong --reps 30 --ns 4 > gpurun_out/s50_sh.txt 2>&1 || { tail -5 gpurun_out/s50_sh.txt; exit 1; }
+    echo "$r $tag $(grep '"streams_req": 0' gpurun_out/s50_sh.txt | cut -c1-75 | tr '\n' ' ')" | tee -a gpurun_out/s50_pool_shape_quarter.txt
+  done; done
+  timeout -k 10 500 python scripts/shard_probe.py --scene caustic --passes 128 --strong --reps 30 > gpurun_out/s50_strong.txt 2>&1 || { tail -5 gpurun_out/s50_strong.txt; exit 1; }
+  grep '"streams_req": 0' gpurun_out/s50_strong.txt | cut -c1-150
+}
+
+s51() {
+  timeout -k 10 300 python -u -m pytest tests/test_gpu_pool.py tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k "pool or auto" > gpurun_out/s51_pytest.log 2>&1 || { tail -30 gpurun_out/s51_pytest.log; exit 1; }
+  tail -1 gpurun_out/s51_pytest.log
+  timeout -k 10 300 python bench.py --workload caustic8 > gpurun_out/s51_bench_caustic8.json 2> gpurun_out/s51_bench_caustic8.err || exit 1
+  tail -1 gpurun_out/s51_bench_caustic8.json | cut -c1-120
+  timeout -k 10 500 python scripts/shard_probe.py --scene caustic --passes 128 --strong --reps 30 > gpurun_out/s51_strong.txt 2>&1 || { tail -5 gpurun_out/s51_strong.txt; exit 1; }
+  grep '"streams_req": 0' gpurun_out/s51_strong.txt | cut -c1-150
+}
+
 case "${1:-}" in
-  s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29|s30|s31|s32|s33|s34|s35|s36|s37|s38|s39|s40|s41|s42|s44|s45|s46|s47|s48) "$1" ;;
-  *) echo "usage: $0 {s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29|s30|s31|s32|s33|s34|s35|s36|s37|s38|s39|s40|s41|s42|s44|s45|s46|s47|s48}"; exit 2 ;;
+  s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29|s30|s31|s32|s33|s34|s35|s36|s37|s38|s39|s40|s41|s42|s44|s45|s46|s47|s48|s49|s50|s51) "$1" ;;
+  *) echo "usage: $0 {s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29|s30|s31|s32|s33|s34|s35|s36|s37|s38|s39|s40|s41|s42|s44|s45|s46|s47|s48|s49|s50|s51}"; exit 2 ;;
 esac
