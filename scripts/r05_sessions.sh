@@ -344,7 +344,15 @@ s51() {
   grep '"streams_req": 0' gpurun_out/s51_strong.txt | cut -c1-150
 }
 
+s52() {
+  for r in 1 2; do for v in "g128r32:BDPT_POOL=32;BDPT_POOL_GRID=128" "g256r32:BDPT_POOL=32;BDPT_POOL_GRID=256" "g128r48:BDPT_POOL=48;BDPT_POOL_GRID=128" "g256r16:BDPT_POOL=16;BDPT_POOL_GRID=256" "g128r24:BDPT_POOL=24;BDPT_POOL_GRID=128"; do
+    tag=${v%%:*}; envs=${v#*:}; IFS=';' read -r -a assign <<< "$envs"
+    env "${assign[@]}" timeout -k 10 300 python scripts/shard_probe.py --scene caustic --passes 128 --strong --reps 30 --ns 2,4 --streams 0 > gpurun_out/s52_sh.txt 2>&1 || { tail -5 gpurun_out/s52_sh.txt; exit 1; }
+    echo "$r $tag $(grep '"streams_req": 0' gpurun_out/s52_sh.txt | cut -c1-75 | tr '\n' ' ')" | tee -a gpurun_out/s52_pool_shape_half_quarter.txt
+  done; done
+}
+
 case "${1:-}" in
-  s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29|s30|s31|s32|s33|s34|s35|s36|s37|s38|s39|s40|s41|s42|s44|s45|s46|s47|s48|s49|s50|s51) "$1" ;;
-  *) echo "usage: $0 {s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29|s30|s31|s32|s33|s34|s35|s36|s37|s38|s39|s40|s41|s42|s44|s45|s46|s47|s48|s49|s50|s51}"; exit 2 ;;
+  s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29|s30|s31|s32|s33|s34|s35|s36|s37|s38|s39|s40|s41|s42|s44|s45|s46|s47|s48|s49|s50|s51|s52) "$1" ;;
+  *) echo "usage: $0 {s9|s10|s11|s12|s13|s14|s16|s17|s18|s19|s20|s21|s22|s23|s24|s27|s28|s29|s30|s31|s32|s33|s34|s35|s36|s37|s38|s39|s40|s41|s42|s44|s45|s46|s47|s48|s49|s50|s51|s52}"; exit 2 ;;
 esac
