@@ -368,6 +368,25 @@ def scaling_breakdown(per_dev, steps, dt, render_s, reduce_s, scaling, passes_pe
     return out
 
 
+def rccl_versions(group=None):
+    """The RCCL libbdpt binds to (bdpt_rccl_version), torch's (torchrun ranks gather over it) and,
+    for an in-process group, bdpt_reduce_info (version, ncclCommCount, devices)."""
+    from gpu_bidirectional_raytracer_amd import _lib
+
+    def fmt(v):
+        return f"{v // 10000}.{v // 100 % 100}.{v % 100}" if isinstance(v, int) and v > 0 else None
+    out = {"libbdpt": fmt(int(_lib.lib.bdpt_rccl_version()))}
+    try:
+        import torch
+        tv = torch.cuda.nccl.version()
+        out["torch"] = ".".join(str(x) for x in tv) if isinstance(tv, tuple) else fmt(tv)
+    except Exception:                                          # noqa: BLE001 (reporting only)
+        out["torch"] = None
+    if group is not None:
+        out["group"] = group.reduce_info
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1,
@@ -387,8 +406,6 @@ def main():
     ap.add_argument("--specialize", type=int, default=1, choices=[0, 1],
                     help="scene-specialised kernels (run-time compiled; results identical)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--tail-seconds", type=float, default=6.0,
-                    help="untimed GPU work after the timed steps (so an outside sampler sees the GPU busy)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-smt-probe", action="store_true", help="skip the SMT-yield probe of the CPU baseline")
     ap.add_argument("--rehearse", action="store_true",
@@ -451,7 +468,7 @@ def main():
     sid, vlp = sched.next(per_step * (untimed + args.steps))
 
     # The CPU baseline (rank 0 at N = 1) runs first, before the GPU is touched: the GPU phase
-    # (tuning, warm-up, timed steps, untimed tail) then runs as one block an outside sampler sees.
+    # (tuning, warm-up, timed steps) then runs as one block.
     cpu = None
     if world == 1 and ndev == 1 and not args.no_cpu_baseline:
         rows = shd.owned_row_ranges(H, rank, nshards, band)
@@ -590,10 +607,14 @@ def main():
     elif mode == "inproc":
         idents = [gpu_identity(d) for d in devices]
     scaling = scaling_breakdown(per_dev, args.steps, dt, render_s, reduce_s, wl["scaling"], per_step)
+    # one kernel for the whole job: every GPU should have adopted the same choice (a share too small
+    # for units runs pass streams; bdpt_host.cpp units_fit) -- say so when they did not
+    kinds = {(tuple(d["mode"]["choice"]), "unit_fold" in d["mode"]["features"],
+              "pixel_pools" in d["mode"]["features"]) for d in per_dev}
+    modes_agree = len(kinds) == 1
+    if not modes_agree and rank == 0:
+        print(f"bench.py: warning: the GPUs ran different kernels: {sorted(kinds)}", file=sys.stderr)
 
-    # Untimed tail: keep the GPU busy for a few seconds after the clock stops, so an outside
-    # utilisation sampler sees the device working (the timed region alone is well under a second
-    # at 1080p).  Its passes are not counted anywhere; the frame is checked below before it runs.
     spp_total = held[0]                                       # passes since the last reset
     if rank == 0:
         # check the (assembled) frame's counters: every rendered pixel holds every pass since the
@@ -605,25 +626,6 @@ def main():
             cnt = r.read_radiance()[1]
         owned = (torch.arange(H).numpy() // band) % nshards < units
         assert (cnt[owned] == spp_total).all() and (cnt[~owned] == 0).all(), "frame counters wrong"
-    tail_s, tail_steps = max(0.0, args.tail_seconds), 0
-    if tail_s > 0:
-        t1 = time.perf_counter()
-        step_s = max(dt / max(args.steps, 1), 1e-4)
-        k = untimed + args.steps
-        tsid, tvlp = sched.next(per_step * 8)                 # the same pass tables, reused per tail step
-        while time.perf_counter() - t1 < tail_s and tail_steps < 100000:
-            burst = max(1, min(8, int((tail_s - (time.perf_counter() - t1)) / step_s) + 1))
-            for _ in range(burst):
-                if held[0] + per_step > COUNTER_CAP:
-                    r.reset_accum()
-                    held[0] = 0
-                r.path_passes(tsid[:per_step], tvlp[:per_step], sync=False)
-                held[0] += per_step
-                tail_steps += 1
-            r.synchronize()
-        barrier()
-        tail_s = time.perf_counter() - t1
-
     if rank == 0:
         w = WORK.get(wl["scene"])
         avg_launch_s = kern_ms / 1e3 / max(launches, 1)
@@ -661,13 +663,18 @@ def main():
             trec = _pmc_record("pmc_traffic.json", args.workload, wl["scene"], W, H, passes_per_launch,
                                r.last_streams, r.last_specialized, kind) if single else None
             skips = [f for f in features if f in ("det_skip", "zero_exit", "last_skip", "bvh")]
-            roofline = {"bound": "valu", "achieved": round(fl, 3), "peak": FP32_NOFMA_TFLOPS, "unit": "TFLOP/s",
-                        "frac": round(fl / FP32_NOFMA_TFLOPS, 4),
+            traffic = trec.get("hbm_bytes_per_launch") if trec else None
+            roofline = {"bound": "valu", "achieved": round(fl, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                        "frac": round(fl / FP32_PEAK_TFLOPS, 4),
                         "frac_spec": round(fl / FP32_PEAK_TFLOPS, 4),
-                        "frac_note": "frac is against the 78.6 T one-op-per-lane-cycle ceiling (no FMA "
-                                     "contraction); frac_spec against the 157.3 TFLOP/s fp32 spec (FMA = 2 FLOP)",
-                        "traffic": trec.get("hbm_bytes_per_launch") if trec else None,
-                        "peak_fma": FP32_PEAK_TFLOPS, "frac_fma": round(fl / FP32_PEAK_TFLOPS, 4),
+                        "frac_issue_ceiling": round(fl / FP32_NOFMA_TFLOPS, 4),
+                        "frac_note": "frac (= frac_spec) is against the 157.3 TFLOP/s fp32 spec (FMA = 2 FLOP); "
+                                     "frac_issue_ceiling against the 78.6 T one-op-per-lane-cycle ceiling that "
+                                     "applies without FMA contraction",
+                        "traffic": traffic,
+                        # calibrated counter bytes per launch / the algorithmic bytes of the same launch:
+                        # > 1 is re-read / partial-line traffic
+                        "traffic_over_model": round(traffic / bytes_per_launch, 3) if traffic else None,
                         "flop_per_sample": round(flop_per_sample(w), 1),
                         "flop_model": "reference-equivalent" if skips else "reference",
                         "kernel_features": features,
@@ -722,14 +729,13 @@ def main():
             "rccl_ranks": world if mode == "ranks" else (ndev if r.reduce_backend == "rccl" else 0),
             "reduce_backend": reduce_backend,
             "reduce_fallback": reduce_fallback,
+            "rccl_version": rccl_versions(r if mode == "inproc" else None),
+            "modes_agree": modes_agree,
             "stream_choice_from": choice_src,
             "devices": [{"rank": q, **idents[q]} for q in range(len(idents))] if mode == "ranks"
             else [{"device": d, **idents[i]} for i, d in enumerate(devices)],
             "device_ms_per_step": round(dev_ms / args.steps, 3),
             "scaling_breakdown": scaling,
-            "untimed_tail": {"seconds": round(tail_s, 2), "steps": tail_steps,
-                             "note": "GPU work after the timed region, not counted: keeps the device visibly "
-                                     "busy for an outside sampler"},
             "roofline": roofline, "cpu_baseline": cpu,
             "host": {"gpu": ident.get("name"), "hostname": socket.gethostname(), "gpu_pci": ident.get("pci"),
                      "gpu_unique_id": ident.get("unique_id")},

@@ -279,6 +279,15 @@ class Renderer:
         """'rccl' / 'peer' for a multi-device context, 'none' for a one-device context."""
         return lib.bdpt_reduce_backend(self._h).decode()
 
+    @property
+    def reduce_info(self) -> str:
+        """The frame reduce in words (bdpt_reduce_info): RCCL version, ranks and devices, or why not RCCL."""
+        buf = ctypes.create_string_buffer(512)
+        n = lib.bdpt_reduce_info(self._h, buf, len(buf))
+        if n < 0:
+            self._chk(n)
+        return buf.value.decode()
+
     def reduce_frame(self) -> None:
         self._chk(lib.bdpt_reduce_frame(self._h))
 

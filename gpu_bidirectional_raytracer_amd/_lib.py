@@ -67,6 +67,8 @@ _SIGS = [
                                           ctypes.c_int, ctypes.c_int, ctypes.c_char_p, _P, ctypes.c_int]),
     ("bdpt_num_devices", ctypes.c_int, [_P]),
     ("bdpt_reduce_backend", ctypes.c_char_p, [_P]),
+    ("bdpt_reduce_info", ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_int]),
+    ("bdpt_rccl_version", ctypes.c_int, []),
     ("bdpt_reduce_frame", ctypes.c_int, [_P]),
     ("bdpt_destroy", None, [_P]),
     ("bdpt_last_error", ctypes.c_char_p, [_P]),

@@ -2,6 +2,8 @@
 //
 // HBM layout (one context = one GPU):
 //   d_rand    float[7,684,096]      MT607 table, lane-major (tid + k*4096)      30.7 MB
+//   d_rndp    float[29][307,364]    the same table in 29 planes (j mod 25)     35.6 MB
+//   d_scp     float2[29][307,364]   {sinf, cosf}(2 pi u) of every d_rndp entry 71.3 MB
 //   d_lp      bdpt_dev_lightpath[4096]  VLPs {hp, rad, nl}, AoS 36 B            147 KB
 //   d_sph     bdpt_dev_sphere[n]    48 B/sphere {p, rad^2, e, rad, c, refl}
 //   d_colors  bdpt_dev_vec[W*H]     running-mean radiance, AoS 12 B (== dev_colors)
@@ -61,6 +63,7 @@ struct bdpt_path_args {
     unsigned emis_mask;             // bit s = sphere s is emissive (sphere counts <= 32)
     const float* rnd;
     const float* rndp;              // the planar copy (BDPT_DEV_RANDP_*), pass-stream kernels
+    const float2* scp;              // per planar entry u: {sinf, cosf}(2 pi u) (bdpt_sincos_planar_kernel)
     const bdpt_dev_lightpath* lp;
     const unsigned* sid;            // per pass (nullptr: the pass table is sid_inl / vlp_inl)
     const int* vlp;                 // per pass

@@ -40,6 +40,7 @@ static_assert(sizeof(bdpt_dev_vec) == sizeof(bdpt_vec), "colour layout");
 
 extern "C" __global__ void bdpt_mt607_kernel(const uint4*, unsigned, float*);
 extern "C" __global__ void bdpt_rand_planar_kernel(const float*, float*);
+extern "C" __global__ void bdpt_sincos_planar_kernel(const float*, float2*);
 extern "C" __global__ void bdpt_light_kernel(const bdpt_dev_sphere*, unsigned, const float*, int,
                                              bdpt_dev_lightpath*);
 extern "C" const void* bdpt_path_kernel_table[36];   // [(S > 1) * 18 + (BVH ? 17 : n <= 16 ? n : 0)]
@@ -159,6 +160,7 @@ struct bdpt_ctx {
     uint4* d_params = nullptr;          // 4096 x {matrix_a, mask_b, mask_c, seed}
     float* d_rand = nullptr;
     float* d_rndp = nullptr;            // planar copy of d_rand (bdpt_rand_planar_kernel)
+    float2* d_scp = nullptr;            // {sinf, cosf}(2 pi u) per d_rndp entry (bdpt_sincos_planar_kernel)
     bdpt_dev_lightpath* d_lp = nullptr;
     bdpt_dev_sphere* d_sph = nullptr;
     unsigned sph_cap = 0;
@@ -203,7 +205,7 @@ struct bdpt_ctx {
     uchar4* d_fpixels = nullptr;
     bdpt_dev_vec* d_ftmp = nullptr;     // peer-copy staging (kReducePeer)
     unsigned* d_ftmpc = nullptr;
-    char reduce_note[160] = {0};        // why RCCL is not used, if it is not
+    char reduce_note[256] = {0};        // the RCCL version and communicator, or why RCCL is not used
     bdpt_cpu_ctx* cpu = nullptr;        // device == BDPT_DEVICE_CPU: the host backend (bdpt_cpu.cpp)
 };
 enum { kReduceNone = 0, kReduceRccl = 1, kReducePeer = 2 };
@@ -324,7 +326,7 @@ static int upload_scene(bdpt_ctx* c) {
 }
 
 static void release(bdpt_ctx* c) {
-    void* bufs[] = {c->d_params, c->d_rand, c->d_rndp, c->d_lp, c->d_sph, c->d_lights, c->d_geom, c->d_lightrec, c->d_colors,
+    void* bufs[] = {c->d_params, c->d_rand, c->d_rndp, c->d_scp, c->d_lp, c->d_sph, c->d_lights, c->d_geom, c->d_lightrec, c->d_colors,
                     c->d_counter, c->d_pixels, c->d_thr, c->d_rbuf, c->d_rmask, c->d_poolctr, c->d_uflags, c->d_uerr, c->d_bvh_nodes,
                     c->d_bvh_geom, c->d_big_geom, c->d_mat, c->d_bvh_ids, c->d_big_ids,
                     c->d_fcolors, c->d_fcounter, c->d_fpixels, c->d_ftmp, c->d_ftmpc};
@@ -841,6 +843,7 @@ int bdpt_create(bdpt_ctx** out, const bdpt_sphere* spheres, unsigned n, int W, i
     CK(hipMalloc(&c->d_params, sizeof(c->h_params)));
     CK(hipMalloc(&c->d_rand, sizeof(float) * BDPT_RAND_N));
     CK(hipMalloc(&c->d_rndp, sizeof(float) * BDPT_DEV_RANDP_PLANES * BDPT_DEV_RANDP_PL));
+    CK(hipMalloc(&c->d_scp, sizeof(float2) * BDPT_DEV_RANDP_PLANES * BDPT_DEV_RANDP_PL));
     CK(hipMalloc(&c->d_lp, sizeof(bdpt_dev_lightpath) * BDPT_LIGHT_POINTS));
     CK(hipMalloc(&c->d_colors, sizeof(bdpt_dev_vec) * np));
     CK(hipMalloc(&c->d_counter, sizeof(unsigned) * np));
@@ -927,6 +930,10 @@ static int one_reset_accum(bdpt_ctx* c) {
     HIPCHK(c, hipSetDevice(c->device));
     if (int rc = join_fold(c)) return rc;
     HIPCHK(c, hipMemsetAsync(c->d_counter, 0, sizeof(unsigned) * (size_t)c->W * c->H, c->stream));
+    if (c->d_uerr) {                                         // a new frame: no stale handover error
+        HIPCHK(c, hipMemsetAsync(c->d_uerr, 0, sizeof(unsigned), c->stream));
+        c->units_check = false;
+    }
     return BDPT_OK;
 }
 
@@ -1024,6 +1031,9 @@ static int one_generate_rand(bdpt_ctx* c, unsigned seed) {
     hipLaunchKernelGGL(bdpt_rand_planar_kernel, dim3((BDPT_DEV_RANDP_PLANES * BDPT_DEV_RANDP_PL + 255) / 256),
                        dim3(256), 0, c->stream, (const float*)c->d_rand, c->d_rndp);
     HIPCHK(c, hipGetLastError());
+    hipLaunchKernelGGL(bdpt_sincos_planar_kernel, dim3((BDPT_DEV_RANDP_PLANES * BDPT_DEV_RANDP_PL + 255) / 256),
+                       dim3(256), 0, c->stream, (const float*)c->d_rndp, c->d_scp);
+    HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->rand_ready = true;
     c->rand_seed = seed;
@@ -1099,6 +1109,7 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
     a.emis_mask = c->emis_mask;
     a.rnd = c->d_rand;
     a.rndp = c->d_rndp;
+    a.scp = c->d_scp;
     a.lp = c->d_lp;
     a.colors = c->d_colors;
     a.counter = c->d_counter;
@@ -1527,19 +1538,27 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
     return BDPT_OK;
 }
 
+// After the stream has drained: did a unit's handover wait time out in a units launch since the
+// last check?  Reported once by whichever call looks first (synchronize, the timing calls, the
+// read-backs); the error word is then cleared, so later launches report only their own timeouts.
+static int units_verdict(bdpt_ctx* c) {
+    if (!c->units_check) return BDPT_OK;
+    unsigned e = 0;
+    HIPCHK(c, hipMemcpy(&e, c->d_uerr, sizeof e, hipMemcpyDeviceToHost));
+    c->units_check = false;
+    if (!e) return BDPT_OK;
+    HIPCHK(c, hipMemset(c->d_uerr, 0, sizeof e));
+    return fail(c, BDPT_EHIP, "path kernel: a unit waited too long for its tile's previous range "
+                              "(its predecessor did not finish within ~1 s; the frame is not valid)");
+}
+
 static int one_synchronize(bdpt_ctx* c) {
     if (!c) return BDPT_EINVAL;
     if (c->cpu) return BDPT_OK;
     HIPCHK(c, hipSetDevice(c->device));
     if (int rc = join_fold(c)) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    if (c->units_check) {                                  // a unit's handover wait timed out?
-        unsigned e = 0;
-        HIPCHK(c, hipMemcpy(&e, c->d_uerr, sizeof e, hipMemcpyDeviceToHost));
-        c->units_check = false;
-        if (e) return fail(c, BDPT_EHIP, "path kernel: a unit waited too long for its tile's previous range "
-                                         "(its predecessor did not finish within ~1 s; the frame is not valid)");
-    }
+    if (int rc = units_verdict(c)) return rc;
     return fold_timing(c);
 }
 
@@ -1581,7 +1600,7 @@ static int one_read_radiance(bdpt_ctx* c, bdpt_vec* colors, unsigned* counter) {
     if (colors) HIPCHK(c, hipMemcpyAsync(colors, c->d_colors, sizeof(bdpt_vec) * np, hipMemcpyDeviceToHost, c->stream));
     if (counter) HIPCHK(c, hipMemcpyAsync(counter, c->d_counter, sizeof(unsigned) * np, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    return BDPT_OK;
+    return units_verdict(c);                                 // a frame known to be invalid is an error
 }
 
 static int one_read_pixels(bdpt_ctx* c, unsigned char* rgba) {
@@ -1594,7 +1613,7 @@ static int one_read_pixels(bdpt_ctx* c, unsigned char* rgba) {
     if (int rc = join_fold(c)) return rc;
     HIPCHK(c, hipMemcpyAsync(rgba, c->d_pixels, 4 * (size_t)c->W * c->H, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    return BDPT_OK;
+    return units_verdict(c);
 }
 
 int bdpt_read_rand(bdpt_ctx* c, float* t) {
@@ -1629,7 +1648,10 @@ static int one_write_lightpaths(bdpt_ctx* c, const bdpt_lightpath* lp) {
         return BDPT_OK;
     }
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipStreamSynchronize(c->stream));             // queued passes may still read dev_lp
+    // queued passes may still read dev_lp: overlapped pooled launches run on the pstreams, which
+    // `stream` follows only through the last fold
+    if (int rc = join_fold(c)) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
     HIPCHK(c, hipMemcpyAsync(c->d_lp, lp, sizeof(bdpt_lightpath) * BDPT_LIGHT_POINTS, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return BDPT_OK;
@@ -1712,6 +1734,7 @@ struct rccl_api {
     decltype(&ncclGroupStart) group_start = nullptr;
     decltype(&ncclGroupEnd) group_end = nullptr;
     decltype(&ncclGetErrorString) errstr = nullptr;
+    decltype(&ncclGetVersion) version = nullptr;       // optional (reporting only)
 };
 
 const rccl_api& rccl() {
@@ -1729,10 +1752,31 @@ const rccl_api& rccl() {
         r.group_start = (decltype(r.group_start))dlsym(h, "ncclGroupStart");
         r.group_end = (decltype(r.group_end))dlsym(h, "ncclGroupEnd");
         r.errstr = (decltype(r.errstr))dlsym(h, "ncclGetErrorString");
+        r.version = (decltype(r.version))dlsym(h, "ncclGetVersion");
         r.ok = r.init_all && r.destroy && r.reduce && r.group_start && r.group_end && r.errstr;
         return r;
     }();
     return api;
+}
+
+// The group bracket of the in-process frame reduce: every device's two ncclReduce calls between
+// one ncclGroupStart and one ncclGroupEnd.  A failed hipSetDevice or ncclReduce stops issuing but
+// still closes the group (an open group would make the next RCCL call on the communicators fail
+// with an unrelated error); the first error is returned in *he / the result.  Templated on the
+// calls so that tests can drive it with injected failures (bdpt__test_reduce_bracket).
+template <class Start, class End, class SetDev, class Reduce>
+ncclResult_t reduce_bracket(int ndev, Start start, End end, SetDev set_device, Reduce reduce, hipError_t* he) {
+    *he = hipSuccess;
+    ncclResult_t r = start();
+    if (r != ncclSuccess) return r;                   // no group was opened
+    for (int k = 0; k < ndev && r == ncclSuccess && *he == hipSuccess; k++) {
+        *he = set_device(k);
+        if (*he != hipSuccess) break;
+        r = reduce(k, 0);                             // colours
+        if (r == ncclSuccess) r = reduce(k, 1);       // counters
+    }
+    const ncclResult_t e = end();                     // always: the group is closed
+    return r != ncclSuccess ? r : e;
 }
 }  // namespace
 
@@ -1786,18 +1830,22 @@ static int assemble(bdpt_ctx* c) {
     }
     if (c->reduce_mode == kReduceRccl) {
         const rccl_api& api = rccl();
-        ncclResult_t r = api.group_start();
-        for (size_t k = 0; r == ncclSuccess && k < c->comms.size(); k++) {
-            bdpt_ctx* d = k == 0 ? c : c->peers[k - 1];
-            HIPCHK(c, hipSetDevice(d->device));
-            r = api.reduce(d->d_colors, k == 0 ? (void*)c->d_fcolors : (void*)d->d_colors, 3 * np, ncclFloat32,
-                           ncclSum, 0, (ncclComm_t)c->comms[k], d->stream);
-            if (r == ncclSuccess)
-                r = api.reduce(d->d_counter, k == 0 ? (void*)c->d_fcounter : (void*)d->d_counter, np, ncclUint32,
-                               ncclSum, 0, (ncclComm_t)c->comms[k], d->stream);
-        }
-        const ncclResult_t e = api.group_end();
-        if (r == ncclSuccess) r = e;
+        auto dev = [&](int k) { return k == 0 ? c : c->peers[k - 1]; };
+        hipError_t he = hipSuccess;
+        const ncclResult_t r = reduce_bracket(
+            (int)c->comms.size(), [&] { return api.group_start(); }, [&] { return api.group_end(); },
+            [&](int k) { return hipSetDevice(dev(k)->device); },
+            [&](int k, int what) {
+                bdpt_ctx* d = dev(k);
+                return what == 0
+                    ? api.reduce(d->d_colors, k == 0 ? (void*)c->d_fcolors : (void*)d->d_colors, 3 * np, ncclFloat32,
+                                 ncclSum, 0, (ncclComm_t)c->comms[k], d->stream)
+                    : api.reduce(d->d_counter, k == 0 ? (void*)c->d_fcounter : (void*)d->d_counter, np, ncclUint32,
+                                 ncclSum, 0, (ncclComm_t)c->comms[k], d->stream);
+            },
+            &he);
+        (void)hipSetDevice(c->device);
+        if (he != hipSuccess) return fail(c, BDPT_EHIP, "frame reduce: hipSetDevice: %s", hipGetErrorString(he));
         if (r != ncclSuccess) return fail(c, BDPT_EHIP, "ncclReduce: %s", api.errstr(r));
         for (size_t k = 1; k < c->comms.size(); k++) {
             HIPCHK(c, hipSetDevice(c->peers[k - 1]->device));
@@ -1878,6 +1926,11 @@ int bdpt_create_multi(bdpt_ctx** out, const bdpt_sphere* spheres, unsigned n, in
         if (r == ncclSuccess) {
             c->comms.assign(comms.begin(), comms.end());
             c->reduce_mode = kReduceRccl;
+            const int v = bdpt_rccl_version();
+            std::string ids;
+            for (int k = 0; k < ndev; k++) ids += (k ? " " : "") + std::to_string(devices[k]);
+            snprintf(c->reduce_note, sizeof c->reduce_note, "rccl %d.%d.%d, ncclCommInitAll: %d ranks on devices [%s]",
+                     v / 10000, v / 100 % 100, v % 100, ndev, ids.c_str());
         } else {
             snprintf(c->reduce_note, sizeof c->reduce_note, "ncclCommInitAll: %s: peer copies", rccl().errstr(r));
         }
@@ -1888,6 +1941,39 @@ int bdpt_create_multi(bdpt_ctx** out, const bdpt_sphere* spheres, unsigned n, in
 }
 
 int bdpt_num_devices(const bdpt_ctx* c) { return c ? 1 + (int)c->peers.size() : BDPT_EINVAL; }
+
+int bdpt_rccl_version(void) {
+    const rccl_api& api = rccl();
+    if (!api.ok) return BDPT_ESTATE;
+    int v = 0;
+    if (!api.version || api.version(&v) != ncclSuccess) return BDPT_ESTATE;
+    return v;
+}
+
+int bdpt_reduce_info(const bdpt_ctx* c, char* buf, int cap) {
+    if (!c || !buf || cap < 1) return BDPT_EINVAL;
+    const char* s = !c->multi ? "none: one device" : c->reduce_note;
+    snprintf(buf, (size_t)cap, "%s", s);
+    return (int)strlen(s);
+}
+
+// Test hook (tests/test_abi_host.py): the reduce bracket driven by fake calls on `ndev` devices,
+// hipSetDevice failing on device `fail_dev` and ncclReduce on call `fail_reduce` (-1: never).
+// Returns the bracket's ncclResult_t; *open_groups = group starts minus ends afterwards (0: the
+// group was closed), *reduces = ncclReduce calls issued, *hip_err = the hipError_t it reported.
+int bdpt__test_reduce_bracket(int ndev, int fail_dev, int fail_reduce, int* open_groups, int* reduces,
+                              int* hip_err) {
+    int open = 0, calls = 0;
+    hipError_t he = hipSuccess;
+    const ncclResult_t r = reduce_bracket(
+        ndev, [&] { open++; return ncclSuccess; }, [&] { open--; return ncclSuccess; },
+        [&](int k) { return k == fail_dev ? hipErrorInvalidDevice : hipSuccess; },
+        [&](int, int) { return calls++ == fail_reduce ? ncclUnhandledCudaError : ncclSuccess; }, &he);
+    if (open_groups) *open_groups = open;
+    if (reduces) *reduces = calls;
+    if (hip_err) *hip_err = (int)he;
+    return (int)r;
+}
 
 const char* bdpt_reduce_backend(const bdpt_ctx* c) {
     if (!c) return "null context";

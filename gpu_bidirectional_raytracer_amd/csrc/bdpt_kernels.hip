@@ -182,16 +182,19 @@ __device__ __forceinline__ unsigned umin3(unsigned a, unsigned b, unsigned c) {
 }
 __device__ __forceinline__ unsigned maxt_key(float maxt) { return maxt > kEps ? key_of(maxt) : 0u; }
 
-// UniformSampleSphereDevice device.cu:157-165
-template <bool TAB = false>
-__device__ __forceinline__ f3 uniform_sphere(float u1, float u2, const double* tab = nullptr) {
+// UniformSampleSphereDevice device.cu:157-165, with s, c = sinf, cosf(2 pi u2) given
+__device__ __forceinline__ f3 uniform_sphere_sc(float u1, float s, float c) {
     const float zz = 1.f - 2.f * u1;
     const float q = 1.f - zz * zz;
     const float r = bdpt_sqrt_rn_core(0.f > q ? 0.f : q);   // q is 0 or >= 2^-24: core is exact
+    return mk(r * c, r * s, zz);
+}
+template <bool TAB = false>
+__device__ __forceinline__ f3 uniform_sphere(float u1, float u2, const double* tab = nullptr) {
     const float phi = 2.f * kPi * u2;
     float s, c;
     sincos_cr<TAB>(phi, &s, &c, tab);
-    return mk(r * c, r * s, zz);
+    return uniform_sphere_sc(u1, s, c);
 }
 
 // Cosine-weighted direction about w (device.cu:676-699; also :190-212 and :357-380).
@@ -216,19 +219,33 @@ __device__ __forceinline__ f3 cosine_dir(f3 w, float u_phi, float u_r2, const do
 // The rest of cosine_dir once u = normalize(cross(a, w)) and r2s = sqrt(r2) are known (the path
 // kernel computes those two on a path shared with refraction): the same operations in the same
 // order as cosine_dir.
-template <bool TAB = false>
-__device__ __forceinline__ f3 cosine_tail(f3 w, f3 u, float u_phi, float u_r2, float r2s,
-                                          const double* tab = nullptr) {
-    const float r1 = 2.f * kPi * u_phi;
+// (s, c = sinf, cosf(2 pi u_phi) given: cosine_tail_sc)
+__device__ __forceinline__ f3 cosine_tail_sc(f3 w, f3 u, float s, float c, float u_r2, float r2s) {
     f3 v = cross(w, u);
-    float s, c;
-    sincos_cr<TAB>(r1, &s, &c, tab);
     u = smul(c * r2s, u);
     v = smul(s * r2s, v);
     f3 nd = add(u, v);
     w = smul(bdpt_sqrt_rn_core(1 - u_r2), w);                // 1 - r2 is 0 or >= 2^-24
     return add(nd, w);
 }
+template <bool TAB = false>
+__device__ __forceinline__ f3 cosine_tail(f3 w, f3 u, float u_phi, float u_r2, float r2s,
+                                          const double* tab = nullptr) {
+    const float r1 = 2.f * kPi * u_phi;
+    float s, c;
+    sincos_cr<TAB>(r1, &s, &c, tab);
+    return cosine_tail_sc(w, u, s, c, u_r2, r2s);
+}
+
+// sinf / cosf of 2 pi u for every entry u of the random table, computed once per table
+// (bdpt_sincos_planar_kernel, planar like d_rndp) instead of per use (BDPT_SCP, pass-stream
+// kernels): the phi of the NEE light sample (u = d_Rand[j + 4], device.cu:162) and of the cosine
+// direction (u = d_Rand[j], :677) are both 2 pi u of a table entry, so the per-vertex fp64 sincos
+// becomes one 8-B load from the same plane offset as the entry itself.  The stored pair is
+// sincos_cr's result for that u, so results are unchanged bit for bit.
+#ifndef BDPT_SCP
+#define BDPT_SCP 1
+#endif
 
 // Fused S = 1 kernel: a lane whose path ends parks until at least BDPT_REGEN_K lanes of its wave
 // (or all of its live lanes) are parked; then they start their next passes together, so the
@@ -316,6 +333,23 @@ extern "C" __global__ __launch_bounds__(256) void bdpt_rand_planar_kernel(const 
     const unsigned p = o / BDPT_DEV_RANDP_PL, q = o - p * BDPT_DEV_RANDP_PL;
     const unsigned src = p < 25u ? 25u * q + p : 25u * (q + 1u) + (p - 25u);
     rndp[o] = src < BDPT_DEV_RAND_N ? rnd[src] : 0.f;
+}
+
+// {sinf, cosf}(2 pi u) for every entry u of the planar copy (BDPT_SCP): the path kernel's own
+// sincos_cr on the same float argument 2.f * kPi * u, with the same LDS table (bdpt_math.h), so
+// each stored pair is what the path kernel would compute for that entry.  7.7 M evaluations
+// per table, once per bdpt_generate_rand.
+extern "C" __global__ __launch_bounds__(256) void bdpt_sincos_planar_kernel(const float* __restrict__ rndp,
+                                                                          float2* __restrict__ scp) {
+    __shared__ double sct[BDPT_SC_N];
+    for (int q = threadIdx.x; q < BDPT_SC_N; q += 256) sct[q] = bdpt_sincos_table_dev[q][0];
+    __syncthreads();
+    const unsigned o = blockIdx.x * 256u + threadIdx.x;
+    if (o >= BDPT_DEV_RANDP_PLANES * BDPT_DEV_RANDP_PL) return;
+    const float x = 2.f * kPi * rndp[o];
+    float s, c;
+    sincos_cr<true>(x, &s, &c, sct);
+    scp[o] = make_float2(s, c);
 }
 
 template <int... S>
@@ -479,6 +513,25 @@ __device__ __forceinline__ void load_rand5p(__amdgpu_buffer_rsrc_t rs, unsigned 
     q4 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, vo, 4 * P4, 0));
 }
 
+// BDPT_SCP: d_Rand[j .. j+3] and {sinf, cosf}(2 pi d_Rand[j]), {sinf, cosf}(2 pi d_Rand[j+4]) --
+// d_Rand[j+4] itself is used only as that angle -- from the planar copies (same plane offsets)
+__device__ __forceinline__ void load_rand_scp(__amdgpu_buffer_rsrc_t rs, __amdgpu_buffer_rsrc_t rsc,
+                                              unsigned j, float& q0, float& q1, float& q2, float& q3,
+                                              float& s0, float& c0, float& s4, float& c4) {
+    typedef unsigned u2v __attribute__((ext_vector_type(2)));
+    const unsigned qd = j / 25u, r = j - qd * 25u;
+    const unsigned e = r * BDPT_DEV_RANDP_PL + qd, vo = e * 4u, vs = e * 8u;
+    constexpr unsigned P4 = BDPT_DEV_RANDP_PL * 4u, P8 = BDPT_DEV_RANDP_PL * 8u;
+    q0 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, vo, 0, 0));
+    q1 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, vo, P4, 0));
+    q2 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, vo, 2 * P4, 0));
+    q3 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, vo, 3 * P4, 0));
+    const u2v a = __builtin_amdgcn_raw_buffer_load_b64(rsc, vs, 0, 0);
+    const u2v b = __builtin_amdgcn_raw_buffer_load_b64(rsc, vs, 4 * P8, 0);
+    s0 = __uint_as_float(a.x); c0 = __uint_as_float(a.y);
+    s4 = __uint_as_float(b.x); c4 = __uint_as_float(b.y);
+}
+
 // f(S), f(S-1), ..., f(0) with compile-time indices while f returns true
 template <int S, typename F>
 __device__ __forceinline__ void unroll_down(F& f) {
@@ -489,7 +542,15 @@ __device__ __forceinline__ void unroll_down(F& f) {
 
 // Handover between the units of a tile (BDPT_UNITS): agent-scope relaxed atomics are coherent
 // across XCDs (sc1 loads / stores on gfx950, no L2 invalidation); the producer waits for its data
-// stores (s_waitcnt vmcnt(0)) before it stores the flag.
+// stores (s_waitcnt vmcnt(0)) before it stores the flag.  Every value handed over (colours,
+// counter, flag) is such an atomic, so no cache maintenance is needed; the C++-model form of the
+// same ordering (BDPT_UNITS_FENCE=1: an agent-scope release fence before the flag store and an
+// acquire fence after the flag load) compiles to buffer_wbl2 sc1 / buffer_inv sc1 -- a write-back
+// and an invalidation of the XCD's whole L2 per unit -- and is kept as a measured variant only
+// ("Units").
+#ifndef BDPT_UNITS_FENCE
+#define BDPT_UNITS_FENCE 0
+#endif
 __device__ __forceinline__ float ld_coherent(float* p) {
     return __uint_as_float(__hip_atomic_load((unsigned*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
@@ -510,7 +571,11 @@ __device__ __forceinline__ void unit_wait(unsigned* f, unsigned want, unsigned* 
         }
         __builtin_amdgcn_s_sleep(10);
     }
+#if BDPT_UNITS_FENCE
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#else
     asm volatile("" ::: "memory");
+#endif
 }
 
 __device__ __forceinline__ void wave_lds_fence() {
@@ -741,13 +806,18 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
     }
     // sin(2pi k/N) for the table-driven sincos (bdpt_math.h; cos is entry k + N/4), 4 KB (2 KB
     // with BDPT_SC_COARSE: every other entry)
+    // (not with BDPT_SCP: the pass-stream kernels load precomputed pairs)
+    constexpr bool kScp = STREAMS && BDPT_SCP;
     constexpr int kSct = BDPT_SC_N >> BDPT_SC_COARSE;
-    __shared__ double sct[kSct];
-    static_assert(kSct % 256 == 0, "table fill");
+    const double* SCT = nullptr;
+    if constexpr (!kScp) {
+        __shared__ double sct[kSct];
+        static_assert(kSct % 256 == 0, "table fill");
 #pragma unroll
-    for (int q = 0; q < kSct; q += 256)
-        sct[q + threadIdx.x] = bdpt_sincos_table_dev[(q + threadIdx.x) << BDPT_SC_COARSE][0];
-    const double* SCT = sct;
+        for (int q = 0; q < kSct; q += 256)
+            sct[q + threadIdx.x] = bdpt_sincos_table_dev[(q + threadIdx.x) << BDPT_SC_COARSE][0];
+        SCT = sct;
+    }
     __syncthreads();
     if (kPool && pool_left == 0u) return;                // uniform: the whole workgroup ends
 
@@ -917,12 +987,12 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
     int k = 0;                        // slot: this lane renders pass s0 + k*S next
     unsigned depth = 0;
     unsigned j = (ibase + SID[k]) % M5;
-    float q0, q1, q2, q3, q4;
+    float q0, q1, q2, q3, q4 = 0.f;
     // one pass per lane (pass streams, S = npass): the lanes of a wave stay on one sid and depth,
     // so their gathers are adjacent in the planar copy (wave-uniform choice)
     // (the fused kernel keeps the linear table: its lanes are on different passes and depths, and
     // planar reads measured -57 % on caustic8, -38 % with whole-wave lockstep groups)
-    const bool planar = STREAMS && a.rndp != nullptr;
+    constexpr bool planar = STREAMS;                 // (the host always passes d_rndp and d_scp)
     constexpr bool kRegen = BDPT_REGEN_K > 1;
     constexpr bool kParkPf = kRegen && !STREAMS;
     // pass streams: a parked lane loads its next pass's first randoms when it parks, with the
@@ -945,7 +1015,15 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
     };
     const __amdgpu_buffer_rsrc_t rsp = __builtin_amdgcn_make_buffer_rsrc(
         (void*)a.rndp, (short)0, (int)(BDPT_DEV_RANDP_PLANES * BDPT_DEV_RANDP_PL * 4u), 0x00020000);
-    if (planar) load_rand5p(rsp, j, q0, q1, q2, q3, q4);
+    // BDPT_SCP: {sinf, cosf}(2 pi d_Rand[j]) and (2 pi d_Rand[j + 4]) (q4 is not loaded)
+    float sn0 = 0.f, cs0 = 0.f, sn4 = 0.f, cs4 = 0.f;
+    const __amdgpu_buffer_rsrc_t rss = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)a.scp, (short)0, (int)(BDPT_DEV_RANDP_PLANES * BDPT_DEV_RANDP_PL * 8u), 0x00020000);
+    auto load_plan = [&](unsigned jj) {
+        if constexpr (kScp) load_rand_scp(rsp, rss, jj, q0, q1, q2, q3, sn0, cs0, sn4, cs4);
+        else load_rand5p(rsp, jj, q0, q1, q2, q3, q4);
+    };
+    if (planar) load_plan(j);
     else
     load_lin(j, q0, q1, q2, q3, q4);
     // BDPT_RNG_PAIR: n0..n4 = the next segment's randoms, loaded with q0..q4 at even depths
@@ -1164,7 +1242,8 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                             specular = false;
                             thr = mul(thr, cc);
                             diff = true;              // shadow rays: below, compacted over the wave
-                            rd = cosine_tail<true>(nl, U, q0, q1, s1, SCT);
+                            if constexpr (kScp) rd = cosine_tail_sc(nl, U, sn0, cs0, q1, s1);
+                            else rd = cosine_tail<true>(nl, U, q0, q1, s1, SCT);
                         } else {
                             const float aa = nt - nc, bb = nt + nc;
                             const float R0 = aa * aa / (bb * bb);
@@ -1189,7 +1268,10 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
         // NEE towards every emitter (same d_Rand[j+3], d_Rand[j+4] for all) + 1 VLP, blended 1/2.
         if (__builtin_amdgcn_ballot_w64(diff) != 0) {
             f3 res = mk(0.f, 0.f, 0.f), usp = res, vsd = res, vcon = res;
-            if (diff) usp = uniform_sphere<true>(q3, q4, SCT);
+            if (diff) {
+                if constexpr (kScp) usp = uniform_sphere_sc(q3, sn4, cs4);
+                else usp = uniform_sphere<true>(q3, q4, SCT);
+            }
             const int nlights = (int)a.n_lights;
             // the emitters' NEE records {p, rad}, {e, (4*pi*rad)*rad} (bdpt_host.cpp upload_scene)
             // through the constant address space (folding them into the specialised build freed
@@ -1411,7 +1493,8 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
         // same registers to wait for -- the compiler otherwise waits for every outstanding memory
         // operation there, the just-issued stores included (their loads completed long before:
         // the shading used them; the wait appeared on paths that skip the shading).
-        if constexpr (STREAMS) asm volatile("" ::"v"(q0), "v"(q1), "v"(q2), "v"(q3), "v"(q4));
+        if constexpr (kScp) asm volatile("" ::"v"(q0), "v"(q1), "v"(q2), "v"(q3), "v"(sn0), "v"(cs0), "v"(sn4), "v"(cs4));
+        else if constexpr (STREAMS) asm volatile("" ::"v"(q0), "v"(q1), "v"(q2), "v"(q3), "v"(q4));
         if (alive) {
             if (!done && ++depth > 6) done = true;                       // :621 7-segment cap
             BDPT_CNT(11, done);
@@ -1476,7 +1559,7 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                 asm volatile("" : "+v"(xyv));
                 const unsigned li = (xyv >> 16) * (unsigned)a.W + (xyv & 0xffffu);
                 j = (26u + li * 25u + depth * 5u + SID[k]) % M5;
-                if (planar) load_rand5p(rsp, j, q0, q1, q2, q3, q4);
+                if (planar) load_plan(j);
                 else
                 {
                 // the camera randoms first: the camera ray waits for them at the top of the loop,
@@ -1516,7 +1599,7 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                 asm volatile("" : "+v"(xyv));
                 const unsigned li = (xyv >> 16) * (unsigned)a.W + (xyv & 0xffffu);
                 j = (26u + li * 25u + depth * 5u + SID[k]) % M5;
-                if (planar) load_rand5p(rsp, j, q0, q1, q2, q3, q4);
+                if (planar) load_plan(j);
                 else
                 load_lin(j, q0, q1, q2, q3, q4);
             }
@@ -1535,7 +1618,7 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                     asm volatile("" : "+v"(xyv));
                     const unsigned li = (xyv >> 16) * (unsigned)a.W + (xyv & 0xffffu);
                     const unsigned jr = (26u + li * 25u + SID[k]) % M5;
-                    if (planar) load_rand5p(rsp, jr, q0, q1, q2, q3, q4);
+                    if (planar) load_plan(jr);
                     else
                     load_lin(jr, q0, q1, q2, q3, q4);
                     if (kPair) load_next(jr);
@@ -1572,7 +1655,11 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
         // pixels once, by the launch's last range: plain stores of several units (on several XCDs,
         // each with its own write-back L2) would reach memory in no defined order
         if (active && s0 + nslot >= a.npass) a.pixels[i] = bdpt_dev_to_rgba(col.x, col.y, col.z, a.gamma_thr);
+#if BDPT_UNITS_FENCE
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+#else
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");          // the stores above are performed
+#endif
         if (lane == 0)
             __hip_atomic_store(a.unit_flags + uflag, a.unit_tag | (urange + 1u), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);

@@ -74,6 +74,13 @@ int  bdpt_create_multi(bdpt_ctx **out, const bdpt_sphere *spheres, unsigned n_sp
 int  bdpt_num_devices(const bdpt_ctx *ctx);
 /* "rccl", "peer", or "none" (a one-device context from bdpt_create). */
 const char *bdpt_reduce_backend(const bdpt_ctx *ctx);
+/* The frame reduce in words, into buf (at most cap bytes, NUL-terminated): for "rccl" the RCCL
+ * version, the rank count ncclCommInitAll was given and the device list; for "peer" why RCCL
+ * is not used.  Returns the full length, BDPT_EINVAL on bad arguments. */
+int  bdpt_reduce_info(const bdpt_ctx *ctx, char *buf, int cap);
+/* ncclGetVersion of the librccl this library binds to (e.g. 22606 = 2.26.6), BDPT_ESTATE if it
+ * cannot be loaded.  Needs no GPU. */
+int  bdpt_rccl_version(void);
 /* Assemble the frame now (otherwise done on the first read-back after a change). */
 int  bdpt_reduce_frame(bdpt_ctx *ctx);
 /* FreeBuffers smallpt_cpu.c:98-110. */
@@ -195,7 +202,11 @@ int  bdpt_last_path_ms(bdpt_ctx *ctx, float *ms);
  * (synchronises first).  reset != 0 zeroes the accumulators after reading them. */
 int  bdpt_path_timing(bdpt_ctx *ctx, double *total_ms, long long *launches, int reset);
 /* Same accumulation, but only the path kernels' own durations (one HIP event pair around each
- * path-kernel launch, excluding the pass-stream fold): what rocprof reports for that kernel. */
+ * path-kernel launch, excluding the pass-stream fold): what rocprof reports for that kernel.
+ * Overlapped pooled launches (pixel pools, BDPT_FEAT_POOLS): consecutive launches run on two
+ * streams and a launch starts while the previous one drains, so their event intervals overlap and
+ * bdpt_last_path_ms, bdpt_path_timing and bdpt_kernel_timing add up to MORE than the wall time;
+ * divide the wall time of a run by its launches for a per-launch rate (bench.py launch_overlap). */
 int  bdpt_kernel_timing(bdpt_ctx *ctx, double *kernel_ms, long long *launches, int reset);
 /* Device k of a (multi-device) context, 0 <= k < bdpt_num_devices (0 = devices[0]): its device
  * id (BDPT_DEVICE_CPU for the host backend), its own path-kernel ms and path ms (with the fold)

@@ -52,6 +52,8 @@ def _load():
     lib.oracle_to_int.restype = ctypes.c_int
     lib.oracle_fnv1a64.argtypes = [P, ctypes.c_uint64]
     lib.oracle_fnv1a64.restype = ctypes.c_uint64
+    lib.oracle_fnv1_64.argtypes = [P, ctypes.c_uint64]
+    lib.oracle_fnv1_64.restype = ctypes.c_uint64
     return lib
 
 
@@ -79,6 +81,12 @@ def mt607(seed: int, params: np.ndarray | None = None) -> np.ndarray:
 def fnv1a64(a: np.ndarray) -> int:
     a = np.ascontiguousarray(a)
     return int(lib.oracle_fnv1a64(_p(a), a.nbytes))
+
+
+def fnv1_64(a) -> int:
+    """FNV-1 (multiply before xor) 64 over the bytes of a (numpy array or bytes)."""
+    a = np.frombuffer(a, np.uint8) if isinstance(a, (bytes, bytearray)) else np.ascontiguousarray(a)
+    return int(lib.oracle_fnv1_64(_p(a), a.nbytes))
 
 
 def light_pass(spheres: np.ndarray, rnd: np.ndarray, current_sample: int = 0,

@@ -584,3 +584,13 @@ uint64_t oracle_fnv1a64(const void *data, uint64_t len)
     for (uint64_t i = 0; i < len; i++) { h ^= p[i]; h *= 0x100000001b3ull; }
     return h;
 }
+
+/* FNV-1 64 (multiply, then xor) over a byte buffer: one of the representations tried against the
+ * survey's digests (tests/golden/fnv_trials.py). */
+uint64_t oracle_fnv1_64(const void *data, uint64_t len)
+{
+    const unsigned char *p = (const unsigned char *)data;
+    uint64_t h = 0xcbf29ce484222325ull;
+    for (uint64_t i = 0; i < len; i++) { h *= 0x100000001b3ull; h ^= p[i]; }
+    return h;
+}

@@ -208,3 +208,34 @@ def test_create_multi_fails_cleanly_without_gpu():
     with pytest.raises(g.BdptError) as e:
         g.Renderer(sp, 17, 9, cam, devices=[0, 1])
     assert e.value.code == _lib.BDPT_EHIP
+
+
+def test_reduce_bracket_closes_the_group_on_every_error():
+    """assemble()'s RCCL group bracket (bdpt_host.cpp reduce_bracket), driven by fake calls with a
+    failing hipSetDevice or ncclReduce injected at every position: the group is always closed
+    (one ncclGroupEnd per ncclGroupStart), issuing stops at the failure, and the failure is
+    reported -- so the context stays usable for the next reduce."""
+    hook = _lib.lib.bdpt__test_reduce_bracket
+    hook.restype, hook.argtypes = ctypes.c_int, [ctypes.c_int] * 3 + [ctypes.POINTER(ctypes.c_int)] * 3
+    for ndev in (1, 2, 8):
+        for fail_dev in range(-1, ndev):
+            for fail_red in range(-1, 2 * ndev):
+                op, nred, herr = ctypes.c_int(9), ctypes.c_int(-1), ctypes.c_int(-1)
+                r = hook(ndev, fail_dev, fail_red, ctypes.byref(op), ctypes.byref(nred), ctypes.byref(herr))
+                assert op.value == 0, (ndev, fail_dev, fail_red)
+                dev_first = fail_dev >= 0 and (fail_red < 0 or fail_red >= 2 * fail_dev)
+                if dev_first:
+                    assert herr.value != 0 and r == 0 and nred.value == 2 * fail_dev
+                elif fail_red >= 0:
+                    assert r != 0 and herr.value == 0 and nred.value == fail_red + 1
+                else:
+                    assert r == 0 and herr.value == 0 and nred.value == 2 * ndev
+
+
+def test_rccl_version_and_reduce_info():
+    v = _lib.lib.bdpt_rccl_version()
+    if v == _lib.BDPT_ESTATE:
+        pytest.skip("librccl not loadable here")
+    assert v >= 20000, v                       # major.minor.patch as m*10000 + n*100 + p
+    buf = ctypes.create_string_buffer(64)
+    assert _lib.lib.bdpt_reduce_info(None, buf, 64) == _lib.BDPT_EINVAL

@@ -120,3 +120,33 @@ def test_pool_counter_cap(gpu, rnd0, monkeypatch):
     assert (cnt == 30000).all()
     ocol, ocnt, _ = _oracle("caustic", W, H, sid, vlp, rnd0)
     assert np.array_equal(col.view(np.uint32), ocol.view(np.uint32))
+
+
+def test_pool_overlapped_launches_then_write_lightpaths(gpu, rnd0, monkeypatch):
+    """bdpt_write_lightpaths right after overlapped pooled launches (they run on the pool streams,
+    which the context's stream follows only through the last fold): the copy must wait for them,
+    so the first call's passes see the old VLPs and the next call's the new ones."""
+    monkeypatch.setenv("BDPT_POOL", "16")
+    W, H, n1, n2 = 161, 97, 256, 32
+    s = g.PassScheduler()
+    s.light()
+    sid, vlp = s.next(n1 + n2)
+    cam, sp = g.read_scene(os.path.join(SCENES, "cornell.scn"))
+    g.update_camera(cam, W, H)
+    with g.Renderer(sp, W, H, cam, device=0) as r:
+        r.set_streams(128)
+        r.light_pass(0)
+        lp1 = r.read_lightpaths()
+        lp2 = lp1.copy()
+        lp2["rad"] *= np.float32(0.5)
+        r.path_passes(sid[:n1], vlp[:n1], sync=False)    # two launches of 128, left running
+        r.write_lightpaths(lp2)
+        r.path_passes(sid[n1:], vlp[n1:])
+        assert "pixel_pools" in r.last_features, r.last_features
+        col, cnt = r.read_radiance()
+    olp = oracle.light_pass(sp, rnd0, 0)
+    assert olp.tobytes() == lp1.tobytes()
+    ocol, ocnt, _ = oracle.path_passes(sp, rnd0, cam, W, H, olp, sid[:n1], vlp[:n1])
+    ocol, ocnt, _ = oracle.path_passes(sp, rnd0, cam, W, H, lp2, sid[n1:], vlp[n1:], colors=ocol, counter=ocnt)
+    assert np.array_equal(cnt, ocnt)
+    assert np.array_equal(col.view(np.uint32), ocol.view(np.uint32))

@@ -107,3 +107,20 @@ def test_oracle_counter_cap():
     col, cnt, _ = oracle.path_passes(sp, rnd, cam, W, H, lp, [1, 2, 3, 4], [1, 1, 2, 2],
                                      colors=col0, counter=cnt0)
     assert (cnt == 30000).all()
+
+
+def test_fnv_trials_record_reproduces():
+    """The survey's FNV digests of the MT table are not reproduced by any byte
+    representation tried (tests/golden/fnv_trials.py); the record of what was tried and what the
+    oracle gives for each must reproduce, so the mismatch stays auditable."""
+    import sys
+    sys.path.insert(0, GOLDEN)
+    import fnv_trials
+    rec = KA["fnv_trials"]
+    got = fnv_trials.trials(0, with_text=False)
+    for k, v in got.items():
+        assert rec["digests"]["0"][k] == v, k
+    assert rec["survey"] == fnv_trials.SURVEY
+    for s in ("0", "5"):
+        assert fnv_trials.SURVEY[s] not in rec["digests"][s].values()
+    assert "none of them" in rec["_note"]

@@ -33,7 +33,7 @@ sys.path.insert(0, os.path.join(REPO, "tools"))
 
 def _sgpr_spills(n, streams):
     if n == -1:
-        return 10 if streams else 2
+        return 11 if streams else 2   # (streams: 10 before the d_scp descriptor, BDPT_SCP)
     return 2 * (n - 10) if n > 10 else 0
 
 
@@ -58,6 +58,7 @@ def test_every_instance_is_present(kernels):
             name = f"_Z18bdpt_path_kernel_tIL{'i' if n >= 0 else 'in'}{abs(n)}ELb{st}EEv14bdpt_path_args"
             assert name in kernels, name
     for k in ("bdpt_mt607_kernel", "bdpt_light_kernel", "bdpt_accum_kernel", "bdpt_rand_planar_kernel",
+              "bdpt_sincos_planar_kernel",
               "bdpt_pixels_kernel", "bdpt_frame_add_kernel"):
         assert k in kernels, k
 
