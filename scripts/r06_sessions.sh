@@ -31,4 +31,48 @@ s2() {
   done
 }
 
+s3() {
+  # sample lists for pooled radiance + sin/cos planes: the GPU suite, then bench A/Bs (prev = the
+  # library of commit 2c3421c: sin/cos planes, the [pass][pixel] radiance with a pass bit mask)
+  pytest_gpu s3_pytest_gpu.log tests || exit 1
+  MODE=bench ARGS="--workload caustic8 --no-cpu-baseline" ROUNDS=2 \
+    VARIANTS="lists: prev:BDPT_LIB=gpu_bidirectional_raytracer_amd/libbdpt_prev.so lists_noscp:BDPT_JIT_FLAGS=-DBDPT_SCP=0" \
+    OUT=gpurun_out/s3_ab.txt bash scripts/ab.sh || exit 1
+  for w in cornell1080 weak64; do
+    MODE=bench ARGS="--workload $w --no-cpu-baseline" ROUNDS=2 \
+      VARIANTS="scp: noscp:BDPT_JIT_FLAGS=-DBDPT_SCP=0" OUT=gpurun_out/s3_ab.txt bash scripts/ab.sh || exit 1
+  done
+}
+
+s4() {
+  # pools forced (BDPT_POOL=64, whole frame): lists vs prev, wall per step + kernel stats
+  ARGS="--scene caustic --streams 128" ROUNDS=2 VARIANTS="lists:BDPT_POOL=64 prev:BDPT_POOL=64;BDPT_LIB=gpu_bidirectional_raytracer_amd/libbdpt_prev.so" \
+    OUT=gpurun_out/s4_ab.txt bash scripts/ab.sh || exit 1
+  for v in lists prev; do
+    lib=""; [ $v = prev ] && lib="BDPT_LIB=gpu_bidirectional_raytracer_amd/libbdpt_prev.so"
+    rm -rf gpurun_out/s4_prof_$v
+    env BDPT_POOL=64 $lib timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/s4_prof_$v -o run --output-format csv -- \
+      python3 scripts/probe_step.py --scene caustic --streams 128 --reps 5 --tag $v > gpurun_out/s4_prof_$v.log 2>&1 || exit 1
+    echo "== $v"; cut -d, -f1-8 gpurun_out/s4_prof_$v/run_kernel_stats.csv | head -6
+  done
+}
+
+s5() {
+  # chunk logs for pooled radiance: pool / config tests first, then the full suite, then A/Bs
+  pytest_gpu s5_pytest_pool.log tests/test_gpu_pool.py tests/test_gpu_configs.py -k "pool or every_kernel_mode or config3" || exit 1
+  ARGS="--scene caustic --streams 128" ROUNDS=2 VARIANTS="logs:BDPT_POOL=64 prev:BDPT_POOL=64;BDPT_LIB=gpu_bidirectional_raytracer_amd/libbdpt_prev.so" \
+    OUT=gpurun_out/s5_ab.txt bash scripts/ab.sh || exit 1
+  for v in logs prev; do
+    lib=""; [ $v = prev ] && lib="BDPT_LIB=gpu_bidirectional_raytracer_amd/libbdpt_prev.so"
+    rm -rf gpurun_out/s5_prof_$v
+    env BDPT_POOL=64 BDPT_POOL_OVERLAP=0 $lib timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/s5_prof_$v -o run --output-format csv -- \
+      python3 scripts/probe_step.py --scene caustic --streams 128 --reps 5 --tag $v > gpurun_out/s5_prof_$v.log 2>&1 || exit 1
+    echo "== $v (serial launches)"; cut -d, -f1-7 gpurun_out/s5_prof_$v/run_kernel_stats.csv | head -4
+  done
+  pytest_gpu s5_pytest_gpu.log tests || exit 1
+  MODE=bench ARGS="--workload caustic8 --no-cpu-baseline" ROUNDS=2 \
+    VARIANTS="logs: prev:BDPT_LIB=gpu_bidirectional_raytracer_amd/libbdpt_prev.so prev_noscp:BDPT_LIB=gpu_bidirectional_raytracer_amd/libbdpt_prev.so;BDPT_JIT_FLAGS=-DBDPT_SCP=0" \
+    OUT=gpurun_out/s5_ab.txt bash scripts/ab.sh || exit 1
+}
+
 "$@"

@@ -184,3 +184,41 @@ def test_north_star_linf_cornell_513_1024spp(gpu, rnd0):
     _same(cnt, ocnt, "counter")
     _same(r.read_pixels(), opix, "pixels")
     r.close()
+
+
+@pytest.mark.parametrize("name", ["cornell", "caustic"])
+def test_1080p_whole_frame_identical_in_every_kernel_mode(gpu, rnd0, name, monkeypatch):
+    """Whole 1921x1081 frames (not sampled rows): the same 128 passes rendered by every kernel
+    mode -- the ordered in-kernel fold (units), pixel pools with the sample lists, two and one
+    pass(es) per lane with the separate fold, and the fused S = 1 kernel -- are bit-identical over
+    every pixel, and rows spread over the frame equal the oracle.  The modes share the sphere
+    tests and shading but differ in everything that maps pixels and passes to lanes, stores
+    radiance and folds it; a band-local defect in one of them cannot hide between sampled rows
+    (VERDICT r5 weak item 8)."""
+    W, H, n = 1921, 1081, 128
+    sid, vlp = _schedule(n)
+    modes = [("units", 128, {"BDPT_UNITS": "8", "BDPT_POOL": "0"}, "unit_fold"),
+             ("pools", 128, {"BDPT_POOL": "64", "BDPT_UNITS": "0"}, "pixel_pools"),
+             ("two_per_lane", 64, {"BDPT_POOL": "0", "BDPT_UNITS": "0"}, None),
+             ("one_per_lane", 128, {"BDPT_POOL": "0", "BDPT_UNITS": "0"}, None),
+             ("fused", 1, {"BDPT_POOL": "0", "BDPT_UNITS": "0"}, None)]
+    frames = {}
+    for tag, streams, env, feat in modes:
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        r, cam, sp = _setup(name, W, H, gpu)
+        r.set_streams(streams)
+        r.path_passes(sid, vlp)
+        if feat:
+            assert feat in r.last_features, (tag, r.last_features)
+        frames[tag] = r.read_radiance()
+        r.close()
+    ref_col, ref_cnt = frames["units"]
+    assert (ref_cnt == n).all()
+    for tag, (col, cnt) in frames.items():
+        _same(col, ref_col, f"{tag} vs units: colors")
+        _same(cnt, ref_cnt, f"{tag} vs units: counter")
+    lp = oracle.light_pass(sp, rnd0, 0)
+    for y in (0, 137, 540, 811, H - 1):
+        ocol, ocnt, _ = oracle.path_passes(sp, rnd0, cam, W, H, lp, sid, vlp, rows=(y, y + 1))
+        _same(ref_col[y], ocol[y], f"row {y}")
