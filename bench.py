@@ -646,11 +646,10 @@ def main():
                 per_unit = max(1.0, passes_per_launch / 8)          # units of a tile per launch
                 bytes_per_launch = own_pixels * (32 * per_unit + 4) + samples_per_launch * 4 * w["rng_reads"]
             elif "pixel_pools" in features:
-                # pixel pools: the counter once per pixel, a 4-B sample-list length per pass and
-                # 32-pixel group; per sample a 16-B record only when its radiance is not +0 (WORK
-                # _nonzero: the oracle's fraction)
+                # pixel pools: the counter and a 16-B pass mask once per pixel; per sample the 12 B
+                # of radiance only when it is not +0 (WORK _nonzero: the oracle's fraction)
                 nz = w.get("_nonzero", 1.0)
-                bytes_per_launch = own_pixels * 4 + samples_per_launch * (4 * w["rng_reads"] + 4 / 32 + 16 * nz)
+                bytes_per_launch = own_pixels * (4 + 16) + samples_per_launch * (4 * w["rng_reads"] + 12 * nz)
             elif r.last_streams > 1:
                 # pass streams: the path kernel reads the counter once and writes 12 B of radiance
                 # per sample; the fold kernel (not this launch) does the colors/pixels RMW

@@ -85,13 +85,8 @@ struct bdpt_path_args {
     int tiles_per_band;             // > 0: grid rows enumerate only this shard's bands
     int streams;                    // pass streams S: lane (pixel, s) renders passes s, s+S, ...
     bdpt_dev_vec* rbuf;             // S > 1: per (pass, launched pixel) radiance, [npass][nloc]
-    // pixel pools: the chunk logs -- per pass and chunk of R x 64 launched pixels the records
-    // {radiance, pixel - chunk start} of its samples that are not +0, in completion order, and
-    // their count (a sample that is not in the log is +0)
-    float4* rrec;                   // [npass][nchunks][R x 64]
-    unsigned* rcnt;                 // [npass][nchunks]
-    int nchunks;                    // ceil(pool_nl / (R x 64))
-    int pool_nl;                    // the launched pixels that lie in the frame (a prefix of the launch)
+    unsigned* rmask;                // pixel pools: per launched pixel 4 words, bit p set = rbuf holds
+                                    // pass p's sample (clear: its radiance is +0, not stored)
     int nloc;                       // launched pixels per pass = tile-grid rows * BDPT_BTH * W
     int pool;                       // > 0 (BDPT_POOL builds): a wave renders one pass, restarting lanes
                                     // on new pixels, claimed in chunks of pool x 64 launched pixels
@@ -156,15 +151,6 @@ __host__ __device__ inline int bdpt_unit_ranges(int npass, int P, int taper) {
         n++;
     }
     return n;
-}
-
-// Pixel pools: part q (0..8) of a pass's nl pixels starts at bdpt_pool_part(nl, q, span), a
-// multiple of the chunk size span = R x 64 (a power of 2), so chunk c of the pass is pixels
-// [c span, (c + 1) span) whichever part it is claimed from.
-__host__ __device__ inline unsigned bdpt_pool_part(unsigned nl, unsigned q, unsigned span) {
-    if (q >= 8u) return nl;
-    const unsigned b = (unsigned)(((unsigned long long)nl * q) >> 3) & ~(span - 1u);
-    return b < nl ? b : nl;
 }
 
 // Tile row of a workgroup row: identity, or the sub-th tile row of this shard's k-th band.

@@ -140,8 +140,7 @@ struct bdpt_ctx {
     bool last_bvh = false;              // the last path-pass launch traversed the BVH
     int cus = 256;                      // compute units (auto stream count)
     bdpt_dev_vec* d_rbuf = nullptr;     // pass-stream radiance, 2 halves of rbuf_cap: [npass][nloc]
-    float4* d_rrec = nullptr;           // pixel pools: chunk-log records, 2 halves of rrec_cap
-    unsigned* d_rcnt = nullptr;         // pixel pools: chunk-log lengths, 2 halves of rlist_cap
+    unsigned* d_rmask = nullptr;        // pixel pools: 4 words per launched pixel (stored passes), 2 halves
     unsigned* d_poolctr = nullptr;      // pixel pools: claimed pixels per pass and eighth, a line each,
                                         // two sets: a pooled launch uses one and zeroes the other
     int pool_set = 0;                   // the set the next pooled launch uses
@@ -157,8 +156,7 @@ struct bdpt_ctx {
     float4 *d_bvh_nodes = nullptr, *d_bvh_geom = nullptr, *d_big_geom = nullptr, *d_mat = nullptr;
     int *d_bvh_ids = nullptr, *d_big_ids = nullptr;
     size_t rbuf_cap = 0;                // elements
-    size_t rlist_cap = 0;               // (pass, chunk) logs a half holds
-    size_t rrec_cap = 0;                // records a half holds
+    size_t rmask_lanes = 0;             // launched pixels the mask halves hold (4 words each)
     uint4* d_params = nullptr;          // 4096 x {matrix_a, mask_b, mask_c, seed}
     float* d_rand = nullptr;
     float* d_rndp = nullptr;            // planar copy of d_rand (bdpt_rand_planar_kernel)
@@ -329,7 +327,7 @@ static int upload_scene(bdpt_ctx* c) {
 
 static void release(bdpt_ctx* c) {
     void* bufs[] = {c->d_params, c->d_rand, c->d_rndp, c->d_scp, c->d_lp, c->d_sph, c->d_lights, c->d_geom, c->d_lightrec, c->d_colors,
-                    c->d_counter, c->d_pixels, c->d_thr, c->d_rbuf, c->d_rrec, c->d_rcnt, c->d_poolctr, c->d_uflags, c->d_uerr, c->d_bvh_nodes,
+                    c->d_counter, c->d_pixels, c->d_thr, c->d_rbuf, c->d_rmask, c->d_poolctr, c->d_uflags, c->d_uerr, c->d_bvh_nodes,
                     c->d_bvh_geom, c->d_big_geom, c->d_mat, c->d_bvh_ids, c->d_big_ids,
                     c->d_fcolors, c->d_fcounter, c->d_fpixels, c->d_ftmp, c->d_ftmpc};
     for (void* b : bufs)
@@ -589,9 +587,7 @@ static void pool_shape(long nloc, bool overlap, int* R, int* G) {
     }
     const int pe = pool_env();
     *G = g;
-    // chunk logs need R x 64 a power of 2 and >= 1024 pixels (bdpt_kernels.hip chunk window):
-    // BDPT_POOL=R is rounded up to 16, 32 or 64
-    *R = pe > 0 ? (pe <= 16 ? 16 : pe <= 32 ? 32 : 64) : r;
+    *R = pe > 0 ? pe : r;
 }
 
 // The specialised kernel for the context's scene and pass-stream mode, compiled on first use;
@@ -1242,13 +1238,9 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
         quarter_ran = quarter && S >= 8;
         S = quarter_ran ? (S + 3) / 4 : (S + 1) / 2;
     }
-    // pixel pools: forced by BDPT_POOL=R, or measured (tuning roles 6, 7) and kept.  Not for
-    // shards whose bands are not whole tile rows: a pool would pass over the other shards' pixels
-    // inside its chunks, and the sample lists need every wave's held pixels to span fewer than 64
-    // consecutive 32-pixel groups (bdpt_kernels.hip gring)
+    // pixel pools: forced by BDPT_POOL=R, or measured (tuning roles 6, 7) and kept
     const int penv = pool_env();
-    const bool want_pool = !bvh && S > 1 && penv != 0 && (c->nshards <= 1 || a.tiles_per_band > 0) &&
-                           lanes < (1L << 26) &&                       // lix keeps a ring entry in bits 26..31
+    const bool want_pool = !bvh && S > 1 && penv != 0 &&
                            (penv > 0 || (c->streams_req == 0 &&
                                          (tune_role == 6 || tune_role == 7 ||
                                           (tune_role < 0 && c->tune_phase == bdpt_ctx::kTunePhases + 1 &&
@@ -1276,56 +1268,30 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
         a.bvh_q = c->bvh_q;
     }
     c->last_bvh = bvh;
-    // pixel pools: the launched pixels that lie in the frame -- a prefix of the launch (the rows
-    // past the frame are the last band's tail) -- so no chunk pixel is ever passed over
-    long pool_nl = 0;
-    for (int r = 0; r < grid_rows * BDPT_BTH; r++) {
-        const int by = r / BDPT_BTH, tpb = a.tiles_per_band;
-        const int tr = tpb <= 0 ? by : tpb == 1 ? c->shard + by * c->nshards
-                                     : (c->shard + (by / tpb) * c->nshards) * tpb + by % tpb;
-        if (tr * BDPT_BTH + r % BDPT_BTH < c->H) pool_nl += c->W;
-    }
-    // chunk-log sizes for any chunk size R x 64 (R = 16..64): logs of 1024 pixels at most, records
-    // of whole chunks
-    const size_t max_chunks = ((size_t)pool_nl + 1023) / 1024;
-    const size_t max_recs = (size_t)pool_nl + 4096;
     if (S > 1 && !want_units) {
         const int cmax = npass < chunk ? npass : chunk;
-        const size_t need = want_pool ? 0 : (size_t)cmax * (size_t)lanes;        // pass streams
-        const size_t lists = want_pool ? (size_t)cmax * max_chunks : 0;          // pools
-        const size_t recs = want_pool ? (size_t)cmax * max_recs : 0;
-        if (need > c->rbuf_cap || lists > c->rlist_cap || recs > c->rrec_cap) {
-            HIPCHK(c, hipStreamSynchronize(c->stream));     // queued passes and folds may use them
+        const size_t need = (size_t)cmax * (size_t)lanes;
+        if (need > c->rbuf_cap || (size_t)lanes > c->rmask_lanes) {
+            HIPCHK(c, hipStreamSynchronize(c->stream));     // queued passes and folds may use it
             HIPCHK(c, hipStreamSynchronize(c->fstream));
             for (hipStream_t ps : c->pstream)
                 if (ps) HIPCHK(c, hipStreamSynchronize(ps));
+            if (c->d_rbuf) HIPCHK(c, hipFree(c->d_rbuf));
+            if (c->d_rmask) HIPCHK(c, hipFree(c->d_rmask));
+            c->d_rbuf = nullptr;
+            c->d_rmask = nullptr;
+            c->rbuf_cap = 0;
             c->rb_used[0] = c->rb_used[1] = false;
-            if (need > c->rbuf_cap) {
-                if (c->d_rbuf) HIPCHK(c, hipFree(c->d_rbuf));
-                c->d_rbuf = nullptr;
-                c->rbuf_cap = 0;
-                if (hipMalloc(&c->d_rbuf, 2 * sizeof(bdpt_dev_vec) * need) != hipSuccess)
-                    return fail(c, BDPT_ENOMEM, "bdpt_path_passes: pass-stream buffer (2 x %zu B)", sizeof(bdpt_dev_vec) * need);
-                c->rbuf_cap = need;
-                // touch every page now (queued before this call's timing event): the first launch
-                // would otherwise pay the first-touch cost, and the stream-mode measurement with it
-                HIPCHK(c, hipMemsetAsync(c->d_rbuf, 0, 2 * sizeof(bdpt_dev_vec) * need, c->stream));
-            }
-            if (lists > c->rlist_cap || recs > c->rrec_cap) {
-                if (c->d_rrec) HIPCHK(c, hipFree(c->d_rrec));
-                if (c->d_rcnt) HIPCHK(c, hipFree(c->d_rcnt));
-                c->d_rrec = nullptr;
-                c->d_rcnt = nullptr;
-                c->rlist_cap = c->rrec_cap = 0;
-                if (hipMalloc(&c->d_rrec, 2 * sizeof(float4) * recs) != hipSuccess)
-                    return fail(c, BDPT_ENOMEM, "bdpt_path_passes: chunk logs (2 x %zu B)", sizeof(float4) * recs);
-                if (hipMalloc(&c->d_rcnt, 2 * sizeof(unsigned) * lists) != hipSuccess)
-                    return fail(c, BDPT_ENOMEM, "bdpt_path_passes: chunk-log lengths (2 x %zu B)", sizeof(unsigned) * lists);
-                c->rlist_cap = lists;
-                c->rrec_cap = recs;
-                HIPCHK(c, hipMemsetAsync(c->d_rrec, 0, 2 * sizeof(float4) * recs, c->stream));
-                HIPCHK(c, hipMemsetAsync(c->d_rcnt, 0, 2 * sizeof(unsigned) * lists, c->stream));
-            }
+            if (hipMalloc(&c->d_rbuf, 2 * sizeof(bdpt_dev_vec) * need) != hipSuccess)
+                return fail(c, BDPT_ENOMEM, "bdpt_path_passes: pass-stream buffer (2 x %zu B)", sizeof(bdpt_dev_vec) * need);
+            if (hipMalloc(&c->d_rmask, 2 * 16 * (size_t)lanes) != hipSuccess)
+                return fail(c, BDPT_ENOMEM, "bdpt_path_passes: pass-stream mask (2 x %zu B)", 16 * (size_t)lanes);
+            c->rmask_lanes = (size_t)lanes;
+            c->rbuf_cap = need;
+            // touch every page now (queued before this call's timing event): the first launch
+            // would otherwise pay the first-touch cost, and the stream-mode measurement with it
+            HIPCHK(c, hipMemsetAsync(c->d_rbuf, 0, 2 * sizeof(bdpt_dev_vec) * need, c->stream));
+            HIPCHK(c, hipMemsetAsync(c->d_rmask, 0, 2 * 16 * (size_t)lanes, c->stream));
         }
     }
     const size_t nchunks = grid_rows > 0 ? (size_t)((npass + chunk - 1) / chunk) : 0;
@@ -1431,14 +1397,15 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
             // the units fold in the kernel: no radiance buffer; the previous call's folds were
             // joined above
             a.rbuf = nullptr;
-            a.rrec = nullptr;
-            a.rcnt = nullptr;
+            a.rmask = nullptr;
         } else if (st) {
             // this half was last read by the fold of the launch before the previous one
             if (c->rb_used[half]) HIPCHK(c, hipStreamWaitEvent(ls, c->rb_fold_ev[half], 0));
-            a.rbuf = jf_pool ? nullptr : c->d_rbuf + (size_t)half * c->rbuf_cap;
-            a.rrec = jf_pool ? c->d_rrec + (size_t)half * c->rrec_cap : nullptr;
-            a.rcnt = jf_pool ? c->d_rcnt + (size_t)half * c->rlist_cap : nullptr;
+            a.rbuf = c->d_rbuf + (size_t)half * c->rbuf_cap;
+            a.rmask = c->d_rmask + (size_t)half * 4 * c->rmask_lanes;
+            // pools mark their stored samples in the mask: cleared first (the fold that read this
+            // half ran earlier on this stream)
+            if (jf_pool) HIPCHK(c, hipMemsetAsync(a.rmask, 0, 16 * (size_t)lanes, ls));
         } else if (int rc = join_fold(c)) {                  // the fused kernel updates colors itself
             return rc;
         }
@@ -1459,18 +1426,6 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
             int R = 1, G = 1;
             pool_shape(lanes, overlap, &R, &G);
             a.pool = R;
-            a.pool_nl = (int)pool_nl;
-            a.nchunks = (int)((pool_nl + 64L * R - 1) / (64L * R));
-            // the log lengths cleared first (the fold that read this half ran earlier on this
-            // stream); logs without records keep length 0
-            HIPCHK(c, hipMemsetAsync(a.rcnt, 0, sizeof(unsigned) * (size_t)a.npass * a.nchunks, ls));
-            // a broken chunk-window assumption is reported like a units handover timeout
-            if (!c->d_uerr) {
-                HIPCHK(c, hipMalloc(&c->d_uerr, sizeof(unsigned) * (32 + 8 * 32)));
-                HIPCHK(c, hipMemsetAsync(c->d_uerr, 0, sizeof(unsigned), c->stream));
-            }
-            a.unit_err = c->d_uerr;
-            c->units_check = true;
             if (overlap) {
                 // set `half`, cleared on this launch's stream (its previous user, the launch two
                 // back, ran earlier on the same stream); the kernel clears no next set
@@ -1539,9 +1494,7 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
         if (st && !unitsl && serial_fold) {                 // the fold after the path kernel
             // (overlapped: after the previous fold too, wherever it ran)
             if (overlap && c->fold_pending) HIPCHK(c, hipStreamWaitEvent(ls, c->rb_fold_ev[c->fold_last], 0));
-            // one workgroup per chunk log, R x 16 threads, the chunk's radiance row in LDS
-            HIPCHK(c, hipLaunchKernel((const void*)&bdpt_accum_serial_kernel, dim3((unsigned)a.nchunks),
-                                      dim3((unsigned)(16 * a.pool)), kargs, sizeof(float) * 3 * 64 * (size_t)a.pool, ls));
+            HIPCHK(c, hipLaunchKernel((const void*)&bdpt_accum_serial_kernel, fgrid, block, kargs, 0, ls));
             if (overlap) {
                 HIPCHK(c, hipEventRecord(c->rb_fold_ev[half], ls));
                 c->rb_used[half] = true;
@@ -1595,9 +1548,6 @@ static int units_verdict(bdpt_ctx* c) {
     c->units_check = false;
     if (!e) return BDPT_OK;
     HIPCHK(c, hipMemset(c->d_uerr, 0, sizeof e));
-    if (e == 2u)
-        return fail(c, BDPT_EHIP, "path kernel: a pool wave held pixels of more than three chunks "
-                                  "(chunk-log window assumption broken; the frame is not valid)");
     return fail(c, BDPT_EHIP, "path kernel: a unit waited too long for its tile's previous range "
                               "(its predecessor did not finish within ~1 s; the frame is not valid)");
 }

@@ -779,8 +779,9 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
     if (kPool && threadIdx.x == 0) pool_left = 0u;
     __syncthreads();
     if (kPool && threadIdx.x < 8u) {
-        const unsigned nl = (unsigned)a.pool_nl, pt = threadIdx.x, span = 64u * (unsigned)a.pool;
-        const unsigned p0 = bdpt_pool_part(nl, pt, span), p1 = bdpt_pool_part(nl, pt + 1u, span);
+        const unsigned nl = (unsigned)a.nloc, pt = threadIdx.x;
+        const unsigned p0 = (unsigned)(((unsigned long long)nl * pt) >> 3);
+        const unsigned p1 = (unsigned)(((unsigned long long)nl * (pt + 1u)) >> 3);
         const unsigned used = __hip_atomic_load(a.pool_ctr + ((unsigned)s0 * 8u + pt) * 32u, __ATOMIC_RELAXED,
                                                 __HIP_MEMORY_SCOPE_AGENT);
         if (p0 + used < p1) atomicOr(&pool_left, 1u);                // LDS
@@ -901,47 +902,22 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
     if (active && a.nshards > 1) active = ((y / a.band_rows) % a.nshards) == a.shard;
     // pixel pools: this wave's chunk is [.., pend) of the launch's row-major pixels (local rows:
     // grid row r of the tile grid is tile row bdpt_dev_tile_row(r)), pcur its next unused pixel,
-    // lix = the lane's pixel (bits 0..29; bits 30..31: the chunk-log slot of its chunk, below)
+    // lix = the lane's pixel
     unsigned lix = 0, pcur = 0, pend = 0;
-    // Chunk logs (the pooled radiance): the samples of pass p whose radiance is not +0 are
-    // appended, as 16-B records {radiance, pixel - chunk start}, to the log of (p, chunk) -- the
-    // chunk the wave drew the pixel from (chunk c = pixels [c R 64, (c + 1) R 64) of the pass) --
-    // and the log's length is rewritten by the wave after every append; the fold then reads each
-    // log once, whole lines.  A wave holds pixels of at most three chunks (a pixel is held for
-    // <= ~14 iterations of <= 64 draws = 896 pixels; chunks are >= 1024 pixels except the
-    // launch's last), kept in four slots used round robin: per slot {start, length, chunk id,
-    // records} in LDS (registers are at the 6-wave bound), a lane's slot in lix's top bits.
-    __shared__ unsigned cst[kPool ? 4 * 16 + 4 : 1];
-    const unsigned cw = __builtin_amdgcn_readfirstlane((unsigned)wave * 16u);   // this wave's slots
-    if (kPool && lane < 16) cst[cw + lane] = 0u;                    // length 0: a free slot
-    if (kPool && lane == 0) cst[64 + wave] = 0u;                    // the next slot to use
     bool drained = false;                              // the pass's pixels are all claimed
     unsigned part = 0, tries = 0;                      // the part claimed from, parts found empty
     if constexpr (kPool) part = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 7u;   // XCC_ID
-    unsigned cslot = 0;                                // the current chunk's slot (uniform)
     auto claim = [&]() -> bool {                       // the next chunk of this wave's pass (uniform)
-        const unsigned span = 64u * (unsigned)a.pool, nl = (unsigned)a.pool_nl;   // R >= 16, a power of 2
+        const unsigned span = 64u * (unsigned)(a.pool > 1 ? a.pool : 1), nl = (unsigned)a.nloc;   // >= 64: claims advance
         while (tries < 8u) {
-            const unsigned p0 = bdpt_pool_part(nl, part, span), p1 = bdpt_pool_part(nl, part + 1u, span);
+            const unsigned p0 = (unsigned)(((unsigned long long)nl * part) >> 3);
+            const unsigned p1 = (unsigned)(((unsigned long long)nl * (part + 1u)) >> 3);
             unsigned b = 0;
             if (lane == 0) b = atomicAdd(a.pool_ctr + ((unsigned)s0 * 8u + part) * 32u, span);
             b = p0 + __builtin_amdgcn_readlane(b, 0);
             if (b < p1) {
                 pcur = b;
                 pend = b + span < p1 ? b + span : p1;
-                // the chunk takes the next slot: {start, length, chunk id, records} (the slot's
-                // previous chunk, four claims back, is complete: the append checks it)
-                if (lane == 0) {
-                    const unsigned sl = cst[64 + wave] & 3u;
-                    unsigned* st = cst + cw + 4u * sl;
-                    st[0] = b;
-                    st[1] = pend - b;
-                    st[2] = b / span;
-                    st[3] = 0u;
-                    cst[64 + wave] = sl + 1u;
-                }
-                wave_lds_fence();
-                cslot = __builtin_amdgcn_readfirstlane((cst[64 + wave] - 1u) & 3u);
                 return true;
             }
             part = (part + 1u) & 7u;
@@ -957,29 +933,15 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
         int lr = (int)((float)q * __builtin_amdgcn_rcpf((float)a.W));
         px = (int)q - lr * a.W;
         if (px < 0) { lr--; px += a.W; } else if (px >= a.W) { lr++; px -= a.W; }
-        // the tile row (bdpt_dev_tile_row) with its division by tiles_per_band through the fp32
-        // reciprocal as well (by < 2^16): a hoisted integer-division reciprocal cost a VGPR
-        const int by = lr / BDPT_BTH, tpb = a.tiles_per_band;
-        int tr = by;
-        if (tpb == 1) {
-            tr = a.shard + by * a.nshards;
-        } else if (tpb > 1) {
-            int kb = (int)((float)by * __builtin_amdgcn_rcpf((float)tpb));
-            int sub = by - kb * tpb;
-            if (sub < 0) { kb--; sub += tpb; } else if (sub >= tpb) { kb++; sub -= tpb; }
-            tr = (a.shard + kb * a.nshards) * tpb + sub;
-        }
-        py = tr * BDPT_BTH + lr % BDPT_BTH;
-        // (pools run only on frames or shards whose bands are whole tile rows, and only over the
-        // launched pixels in the frame: bdpt_host.cpp want_pool, pool_nl)
-        return py < a.H;
+        py = bdpt_dev_tile_row(a, lr / BDPT_BTH) * BDPT_BTH + lr % BDPT_BTH;
+        if (py >= a.H) return false;
+        return a.nshards <= 1 || a.tiles_per_band > 0 || ((py / a.band_rows) % a.nshards) == a.shard;
     };
     if constexpr (kPool) {
         active = claim();
         lix = pcur + (unsigned)lane;
         pcur += 64u;
         if (active) active = pool_pixel(lix, x, y);
-        lix |= cslot << 30;
     }
     // Pass p = s0 + k*S (slot k) is rendered iff counter0 + p < 30000 (one increment per pass).
     float4* SQ = Q + wave * kQueue * 2;
@@ -1075,7 +1037,6 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
     if constexpr (kParkPf) load_cam(j);
     f3 ro = mk(0.f, 0.f, 0.f), rd = ro, thr = ro, rad = ro, nl = ro;
     bool specular = true, fresh = true, parked = false, want = kPool && !active;
-    bool pstore = false;                              // pools: this lane's sample goes to its chunk log
     bool alive = active && nslot > 0 && cnt0 + (unsigned)(kUnits ? k : s0 + k * S) < BDPT_DEV_COUNTER_CAP;
 
     // (a pool lane without a pixel yet keeps the loop going: it draws one at the iteration's end)
@@ -1555,16 +1516,21 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                     r.x = rad.x; r.y = rad.y; r.z = rad.z;
                     unsigned xyv = xy;
                     asm volatile("" : "+v"(xyv));
+                    const int li = kPool ? (int)lix : ((int)(xyv >> 16) - yoff) * a.W + (int)(xyv & 0xffffu);
+                    const size_t ri = (size_t)(s0 + k * S) * a.nloc + (size_t)li;
                     if constexpr (kPool) {
                         // sparse radiance: pixel pools serve open scenes, where most samples are
                         // exactly +0 (caustic: 78 % of the samples, half of all 64-pixel runs) --
-                        // only the others are stored (every bit +0 counts as zero, so a -0
-                        // component is stored and folded as it is), appended to their chunk's
-                        // log after this block, where the wave is converged (pstore)
-                        pstore = (__float_as_uint(r.x) | __float_as_uint(r.y) | __float_as_uint(r.z)) != 0u;
+                        // only the others are stored, each marking its pass in the pixel's mask
+                        // (zeroed before the launch), and the fold reads only those (every bit +0
+                        // counts as zero, so a -0 component is stored and folded as it is)
+                        if ((__float_as_uint(r.x) | __float_as_uint(r.y) | __float_as_uint(r.z)) != 0u) {
+                            a.rbuf[ri] = r;
+                            const unsigned pq = (unsigned)(s0 + k * S);
+                            atomicOr(a.rmask + (size_t)li * 4u + (pq >> 5), 1u << (pq & 31u));
+                        }
                     } else {
-                        const int li = ((int)(xyv >> 16) - yoff) * a.W + (int)(xyv & 0xffffu);
-                        a.rbuf[(size_t)(s0 + k * S) * a.nloc + (size_t)li] = r;
+                        a.rbuf[ri] = r;
                     }
                 }
                 fresh = true;
@@ -1607,31 +1573,6 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
             }
         }
         if constexpr (kPool) {
-            // append this iteration's stored samples to their chunk logs: a position from the
-            // slot's record counter (LDS atomic), then the 16-B record; lane 0 rewrites the
-            // lengths of the wave's live logs (one work-item's stores to a word land in program
-            // order, so the last length written is the log's final length)
-            if (__builtin_amdgcn_ballot_w64(pstore) != 0) {
-                if (pstore) {
-                    unsigned* st = cst + cw + 4u * (lix >> 30);
-                    const unsigned pos = atomicAdd(st + 3, 1u);
-                    const unsigned pl = (lix & 0x3fffffffu) - st[0];
-                    // the slot still holds the lane's chunk (else a fourth chunk reused it while
-                    // the lane held a pixel: the window assumption broke -- reported, not hidden)
-                    const unsigned span = 64u * (unsigned)a.pool;
-                    const size_t lg = (size_t)(unsigned)s0 * (unsigned)a.nchunks + st[2];
-                    if (pl < st[1] && pos < st[1])
-                        a.rrec[lg * span + pos] = make_float4(rad.x, rad.y, rad.z, __uint_as_float(pl));
-                    else
-                        __hip_atomic_store(a.unit_err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-                wave_lds_fence();
-                if (lane < 4) {
-                    const unsigned* st = cst + cw + 4u * (unsigned)lane;
-                    if (st[1] != 0u) a.rcnt[(size_t)(unsigned)s0 * (unsigned)a.nchunks + st[2]] = st[3];
-                }
-                pstore = false;
-            }
             // lanes whose path ended take the next pixels of the wave's pool, in lane order (a
             // pixel outside the frame or the shard is passed over: the lane draws again)
             unsigned long long mw = __builtin_amdgcn_ballot_w64(want);
@@ -1642,7 +1583,7 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                 int px = 0, py = 0;
                 if (want && pool_pixel(q, px, py)) {
                     want = false;
-                    lix = q | (cslot << 30);
+                    lix = q;
                     xy = ((unsigned)py << 16) | (unsigned)px;
                     camb[threadIdx.x] = make_double2((double)((float)px * a.inv_w) - a.half_w,
                                                      (double)((float)py * a.inv_h) - a.half_h);
@@ -1750,155 +1691,86 @@ extern "C" const void* bdpt_path_kernel_table[36] = {BDPT_ROW(false), BDPT_ROW(t
 // rows, so a wave reads 768 contiguous bytes per pass (on the path launch's 8x8 wave tiles it
 // read 8 runs of 96 B: caustic8 -1.9 to -3.7 %, cornell S = 64 -0.3 %, weak64 +-0.2 %,
 // profiles/r05_s16_fold_rows_ab.txt).
-__device__ __forceinline__ void accum_fold(bdpt_dev_vec& col, unsigned& cnt, const bdpt_dev_vec& r) {
-    if (cnt == 0) {
-        col = r;
-    } else {
-        const float k1 = (float)cnt;
-        const float k2 = rcp_rn_inrange(k1 + 1.f);            // 2 <= k1 + 1 <= 30000: exact
-        col.x = (col.x * k1 + r.x) * k2;
-        col.y = (col.y * k1 + r.y) * k2;
-        col.z = (col.z * k1 + r.z) * k2;
-    }
-    cnt++;
-}
-
-// The launched pixel l's frame position; false for rows past the frame or of other shards.
-__device__ __forceinline__ bool accum_pixel(const bdpt_path_args& a, long l, int* i) {
-    if (l >= a.nloc) return false;
+template <int U, bool SPARSE>
+__device__ __forceinline__ void accum_body(const bdpt_path_args& a) {
+    const long l = (long)blockIdx.x * 256 + threadIdx.x;
+    if (l >= a.nloc) return;
     const int ly = (int)(l / a.W);
     const int x = (int)(l - (long)ly * a.W);
     const int y = bdpt_dev_tile_row(a, ly / BDPT_BTH) * BDPT_BTH + ly % BDPT_BTH;
-    if (y >= a.H) return false;
-    if (a.nshards > 1 && ((y / a.band_rows) % a.nshards) != a.shard) return false;
-    *i = y * a.W + x;
-    return true;
-}
-
-// passes that count for a pixel with counter cnt0: p < npass with cnt0 + p < 30000 (the path
-// kernel rendered exactly these)
-__device__ __forceinline__ int accum_passes(const bdpt_path_args& a, unsigned cnt0) {
-    return cnt0 >= BDPT_DEV_COUNTER_CAP ? 0
-         : (int)(BDPT_DEV_COUNTER_CAP - cnt0 < (unsigned)a.npass ? BDPT_DEV_COUNTER_CAP - cnt0 : (unsigned)a.npass);
-}
-
-// Pass streams: rbuf[0..npass) of the pixel folded in pass order.  (Folds with 8 loads in flight, or
-// with streaming loads, ran faster alone but slowed the concurrent path kernel more: caustic8
-// -1.3 % (round 2), -4 to -13 % (profiles/r05_s3_*).)
-__device__ __forceinline__ void accum_body(const bdpt_path_args& a) {
-    const long l = (long)blockIdx.x * 256 + threadIdx.x;
-    int i = 0;
-    if (!accum_pixel(a, l, &i)) return;
+    if (y >= a.H) return;
+    if (a.nshards > 1 && ((y / a.band_rows) % a.nshards) != a.shard) return;
+    const int i = y * a.W + x;
+    const size_t li = (size_t)ly * a.W + x;
     const unsigned cnt0 = a.counter[i];
     unsigned cnt = cnt0;
     bdpt_dev_vec col = a.colors[i];
-    const int n = accum_passes(a, cnt0);
-    const bdpt_dev_vec* __restrict__ rb = a.rbuf + l;
-    for (int p = 0; p < n; p++) accum_fold(col, cnt, rb[(size_t)p * a.nloc]);
+    // passes that count: p < npass with cnt0 + p < 30000 (the path kernel rendered exactly these)
+    const int n = cnt0 >= BDPT_DEV_COUNTER_CAP ? 0
+                : (int)(BDPT_DEV_COUNTER_CAP - cnt0 < (unsigned)a.npass ? BDPT_DEV_COUNTER_CAP - cnt0 : (unsigned)a.npass);
+    const bdpt_dev_vec* __restrict__ rb = a.rbuf + li;
+    unsigned m0 = 0u, m1 = 0u, m2 = 0u, m3 = 0u;                 // SPARSE: which passes are stored
+    if constexpr (SPARSE) {
+        const uint4 mw = reinterpret_cast<const uint4*>(a.rmask)[li];
+        m0 = mw.x; m1 = mw.y; m2 = mw.z; m3 = mw.w;
+    }
+    // (the load under a branch, component by component: `stored ? rb[q] : zero` on the struct
+    // became a load through a selected pointer, with `zero` on the stack)
+    auto sample = [&](int q, bool stored) -> bdpt_dev_vec {
+        bdpt_dev_vec v;
+        v.x = v.y = v.z = 0.f;
+        if (stored) {
+            const bdpt_dev_vec* e = rb + (size_t)q * a.nloc;
+            v.x = e->x;
+            v.y = e->y;
+            v.z = e->z;
+        }
+        return v;
+    };
+    auto fold = [&](const bdpt_dev_vec& r) {
+        if (cnt == 0) {
+            col = r;
+        } else {
+            const float k1 = (float)cnt;
+            const float k2 = rcp_rn_inrange(k1 + 1.f);        // 2 <= k1 + 1 <= 30000: exact
+            col.x = (col.x * k1 + r.x) * k2;
+            col.y = (col.y * k1 + r.y) * k2;
+            col.z = (col.z * k1 + r.z) * k2;
+        }
+        cnt++;
+    };
+    // (folds with 8 loads in flight, or with streaming loads, ran faster alone but slowed the
+    // concurrent path kernel more: caustic8 -1.3 % (round 2), -4 to -13 % (profiles/r05_s3_*))
+    int p = 0;
+    if constexpr (U > 1) {                   // U loads in flight (the fold after the path kernel)
+        for (; p + U <= n; p += U) {
+            bdpt_dev_vec v[U];
+            if constexpr (SPARSE) {
+                const unsigned w = p < 64 ? (p < 32 ? m0 : m1) : (p < 96 ? m2 : m3);
+                const unsigned bits = w >> (p & 31);              // p is a multiple of U = 16
+#pragma unroll
+                for (int u = 0; u < U; u++) v[u] = sample(p + u, (bits >> u) & 1u);
+            } else {
+#pragma unroll
+                for (int u = 0; u < U; u++) v[u] = sample(p + u, true);
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++) fold(v[u]);
+        }
+    }
+    for (; p < n; p++) {
+        const unsigned w = p < 64 ? (p < 32 ? m0 : m1) : (p < 96 ? m2 : m3);
+        fold(sample(p, !SPARSE || ((w >> (p & 31)) & 1u)));
+    }
     if (cnt == cnt0) return;
     a.colors[i] = col;
     a.counter[i] = cnt;
     a.pixels[i] = bdpt_dev_to_rgba(col.x, col.y, col.z, a.gamma_thr);
 }
-extern "C" __global__ __launch_bounds__(256) void bdpt_accum_kernel(bdpt_path_args a) { accum_body(a); }
-
-// Pixel pools: the fold over the chunk logs, after the path kernel on its stream.  One workgroup
-// per chunk of span = R x 64 launched pixels, span / 4 threads, four pixels per thread (pixel
-// j = t + m span / 4) with their running means in registers.  Per pass (in order): the log's
-// records are scattered into an LDS radiance row (+0 where no record), every pixel folds its
-// entry, and the written entries are cleared again; the next pass's records are loaded while
-// this one is folded.  Log lengths of all passes are staged in LDS first.
-__device__ __forceinline__ void accum_chunks_body(const bdpt_path_args& a) {
-    extern __shared__ float4 xdyn[];
-    float* xb = (float*)xdyn;                                   // [3][span]
-    __shared__ unsigned lens[BDPT_DEV_INLINE_PASSES];
-    const unsigned span = 64u * (unsigned)a.pool, T = span / 4u, t = threadIdx.x;
-    const unsigned c = blockIdx.x, nc = (unsigned)a.nchunks;
-    const unsigned cstart = c * span;
-    for (unsigned q = t; q < (unsigned)a.npass; q += T) lens[q] = a.rcnt[(size_t)q * nc + c];
-    for (unsigned q = t; q < 3u * span; q += T) xb[q] = 0.f;
-    bdpt_dev_vec col[4];
-    unsigned cnt[4], cnt0[4];
-    int fi[4];
-#pragma unroll
-    for (int m = 0; m < 4; m++) {
-        const unsigned l = cstart + t + (unsigned)m * T;
-        fi[m] = -1;
-        int i = 0;
-        cnt0[m] = BDPT_DEV_COUNTER_CAP;                        // not a frame pixel: never folds
-        col[m].x = col[m].y = col[m].z = 0.f;
-        if (l < (unsigned)a.pool_nl && accum_pixel(a, (long)l, &i)) {
-            fi[m] = i;
-            cnt0[m] = a.counter[i];
-            col[m] = a.colors[i];
-        }
-        cnt[m] = cnt0[m];
-    }
-    __syncthreads();
-    const float4* __restrict__ recs = a.rrec;
-    auto load = [&](int p, float4 (&rv)[4], unsigned& n) {
-        n = p < a.npass ? lens[p] : 0u;
-        n = n < span ? n : span;                                // (a log never exceeds its chunk)
-        const size_t base = ((size_t)(unsigned)p * nc + c) * span;
-#pragma unroll
-        for (int m = 0; m < 4; m++)
-            if (t + (unsigned)m * T < n) rv[m] = recs[base + t + (unsigned)m * T];
-    };
-    float4 cur[4], nxt[4];
-    unsigned ncur = 0, nnxt = 0;
-    load(0, cur, ncur);
-    for (int p = 0; p < a.npass; p++) {                         // uniform
-        if (p + 1 < a.npass) load(p + 1, nxt, nnxt);
-        if (ncur != 0u) {
-#pragma unroll
-            for (int m = 0; m < 4; m++)
-                if (t + (unsigned)m * T < ncur) {
-                    const unsigned pl = __float_as_uint(cur[m].w) & (span - 1u);
-                    xb[pl] = cur[m].x;
-                    xb[span + pl] = cur[m].y;
-                    xb[2u * span + pl] = cur[m].z;
-                }
-            __syncthreads();
-        }
-#pragma unroll
-        for (int m = 0; m < 4; m++) {
-            if (cnt[m] < BDPT_DEV_COUNTER_CAP) {                // p < the pixel's passes (cap)
-                const unsigned j = t + (unsigned)m * T;
-                bdpt_dev_vec r;
-                r.x = r.y = r.z = 0.f;
-                if (ncur != 0u) {
-                    r.x = xb[j];
-                    r.y = xb[span + j];
-                    r.z = xb[2u * span + j];
-                }
-                accum_fold(col[m], cnt[m], r);
-            }
-        }
-        if (ncur != 0u) {
-            __syncthreads();
-#pragma unroll
-            for (int m = 0; m < 4; m++)
-                if (t + (unsigned)m * T < ncur) {
-                    const unsigned pl = __float_as_uint(cur[m].w) & (span - 1u);
-                    xb[pl] = 0.f;
-                    xb[span + pl] = 0.f;
-                    xb[2u * span + pl] = 0.f;
-                }
-            __syncthreads();
-        }
-#pragma unroll
-        for (int m = 0; m < 4; m++) cur[m] = nxt[m];
-        ncur = nnxt;
-    }
-#pragma unroll
-    for (int m = 0; m < 4; m++) {
-        if (fi[m] < 0 || cnt[m] == cnt0[m]) continue;
-        a.colors[fi[m]] = col[m];
-        a.counter[fi[m]] = cnt[m];
-        a.pixels[fi[m]] = bdpt_dev_to_rgba(col[m].x, col[m].y, col[m].z, a.gamma_thr);
-    }
-}
-extern "C" __global__ __launch_bounds__(1024) void bdpt_accum_serial_kernel(bdpt_path_args a) { accum_chunks_body(a); }
+extern "C" __global__ __launch_bounds__(256) void bdpt_accum_kernel(bdpt_path_args a) { accum_body<1, false>(a); }
+// pixel pools: after the path kernel, on its stream, over the sparse radiance
+extern "C" __global__ __launch_bounds__(256) void bdpt_accum_serial_kernel(bdpt_path_args a) { accum_body<16, true>(a); }
+// (8 or 32 samples in flight per thread measured the same or 0.5 % slower, profiles/r05_s27_fold_u.txt)
 
 // Frame assembly of a multi-device context without RCCL: add a peer's zero-padded frame (exact:
 // each pixel is non-zero on one device only, and x + 0 == x).

@@ -75,4 +75,21 @@ s5() {
     OUT=gpurun_out/s5_ab.txt bash scripts/ab.sh || exit 1
 }
 
+s6() {
+  # the multi-device abort (s1, s5: in bdpt_create_multi, intermittent): the test alone, verbose,
+  # RCCL warnings on; then the chunk logs (lengths at slot reuse, one-barrier fold) vs prev
+  NCCL_DEBUG=WARN timeout -k 10 300 python -u -m pytest tests/test_gpu_multi.py -m gpu -x -v -s --timeout 120 --timeout-method thread > gpurun_out/s6_multi.log 2>&1 || { grep -v "^  File" gpurun_out/s6_multi.log | tail -40; exit 1; }
+  tail -2 gpurun_out/s6_multi.log
+  pytest_gpu s6_pytest_pool.log tests/test_gpu_pool.py tests/test_gpu_configs.py -k "pool or every_kernel_mode or config3" || exit 1
+  ARGS="--scene caustic --streams 128" ROUNDS=2 VARIANTS="logs64:BDPT_POOL=64 logs32:BDPT_POOL=32 prev:BDPT_POOL=64;BDPT_LIB=gpu_bidirectional_raytracer_amd/libbdpt_prev.so" \
+    OUT=gpurun_out/s6_ab.txt bash scripts/ab.sh || exit 1
+  for v in logs prev; do
+    lib=""; [ $v = prev ] && lib="BDPT_LIB=gpu_bidirectional_raytracer_amd/libbdpt_prev.so"
+    rm -rf gpurun_out/s6_prof_$v
+    env BDPT_POOL=64 BDPT_POOL_OVERLAP=0 $lib timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/s6_prof_$v -o run --output-format csv -- \
+      python3 scripts/probe_step.py --scene caustic --streams 128 --reps 5 --tag $v > gpurun_out/s6_prof_$v.log 2>&1 || exit 1
+    echo "== $v (serial launches)"; cut -d, -f1-7 gpurun_out/s6_prof_$v/run_kernel_stats.csv | head -4
+  done
+}
+
 "$@"

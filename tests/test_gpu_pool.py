@@ -4,9 +4,8 @@ it, claimed in chunks of R x 64 from the pass's eight counters (BDPT_POOL_GRID=G
 per wave and pass).  Every pixel must still get exactly its passes, in pass order through the
 fold, so the frame is the oracle's bit for bit -- whole frames, two calls (the counters carry
 over), chunks larger than the frame, more waves than chunks (waves that find their pass
-drained), and shards whose bands are whole tile rows (the grid enumerates only them); shards
-whose bands are not whole tile rows do not get pools (a chunk would pass over the other shards'
-pixels, which the sample lists do not allow: bdpt_host.cpp want_pool) and must still be exact."""
+drained), and shards whose bands are whole tile rows (the grid enumerates only them) or not
+(pixels of other shards inside a chunk are passed over)."""
 import os
 
 import numpy as np
@@ -31,7 +30,7 @@ def _oracle(name, W, H, sid, vlp, rnd0):
     return oracle.path_passes(sp, rnd0, cam, W, H, lp, sid, vlp)
 
 
-def _render(name, W, H, sid, vlp, split, shard=None, pools=True):
+def _render(name, W, H, sid, vlp, split, shard=None):
     cam, sp = g.read_scene(os.path.join(SCENES, name + ".scn"))
     g.update_camera(cam, W, H)
     with g.Renderer(sp, W, H, cam, device=0) as r:
@@ -42,7 +41,7 @@ def _render(name, W, H, sid, vlp, split, shard=None, pools=True):
         r.path_passes(sid[:split], vlp[:split])
         r.path_passes(sid[split:], vlp[split:])
         assert r.last_streams > 1 and r.last_specialized, r.specialize_status
-        assert ("pixel_pools" in r.last_features) == pools, r.last_features
+        assert "pixel_pools" in r.last_features, r.last_features
         col, cnt = r.read_radiance()
         px = r.read_pixels()
     return col, cnt, px
@@ -72,7 +71,7 @@ def test_pool_shard_matches_oracle(gpu, rnd0, band, monkeypatch):
     s = g.PassScheduler()
     s.light()
     sid, vlp = s.next(npass)
-    col, cnt, px = _render("cornell", W, H, sid, vlp, 5, shard=(rank, N, band), pools=band % 8 == 0)
+    col, cnt, px = _render("cornell", W, H, sid, vlp, 5, shard=(rank, N, band))
     ocol, ocnt, opx = _oracle("cornell", W, H, sid, vlp, rnd0)
     owned = (np.arange(H) // band) % N == rank
     assert (cnt[owned] == npass).all() and (cnt[~owned] == 0).all() and (col[~owned] == 0).all()
