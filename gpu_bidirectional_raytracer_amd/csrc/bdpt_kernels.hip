@@ -806,8 +806,10 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
     }
     // sin(2pi k/N) for the table-driven sincos (bdpt_math.h; cos is entry k + N/4), 4 KB (2 KB
     // with BDPT_SC_COARSE: every other entry)
-    // (not with BDPT_SCP: the pass-stream kernels load precomputed pairs)
-    constexpr bool kScp = STREAMS && BDPT_SCP;
+    // (not with BDPT_SCP: the pass-stream kernels load precomputed pairs -- except the pixel-pool
+    // build, whose restarted lanes are bound by their random-table gathers: the two extra gathers
+    // per segment cost caustic8 2.5 %, one-session A/B profiles/r06_s8_ab_scp_caustic8.txt)
+    constexpr bool kScp = STREAMS && BDPT_SCP && !BDPT_POOL;
     constexpr int kSct = BDPT_SC_N >> BDPT_SC_COARSE;
     const double* SCT = nullptr;
     if constexpr (!kScp) {

@@ -92,4 +92,41 @@ s6() {
   done
 }
 
+s7() {
+  # the multi-device abort: a stress loop of bdpt_create_multi([0]) with RCCL warnings on, then the
+  # full suite with output uncaptured (-s) so an abort's stderr is kept; then the reverted pools
+  NCCL_DEBUG=WARN timeout -k 10 240 python -u scripts/multi_stress.py --n 60 > gpurun_out/s7_stress.log 2>&1 || { tail -30 gpurun_out/s7_stress.log; exit 1; }
+  tail -2 gpurun_out/s7_stress.log
+  NCCL_DEBUG=WARN timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -s --timeout 300 --timeout-method thread > gpurun_out/s7_pytest_gpu.log 2>&1 || { grep -v "^  File" gpurun_out/s7_pytest_gpu.log | tail -60; exit 1; }
+  grep -c PASSED gpurun_out/s7_pytest_gpu.log; tail -1 gpurun_out/s7_pytest_gpu.log
+}
+
+s8() {
+  # final build: the multi tests (RCCL group case in a child), A/Bs (sin/cos planes on caustic8,
+  # the release/acquire handover variant of units), caustic8 strong-scaling shares, final benches
+  pytest_gpu s8_pytest_multi.log tests/test_gpu_multi.py || exit 1
+  MODE=bench ARGS="--workload caustic8 --no-cpu-baseline" ROUNDS=2 \
+    VARIANTS="scp: noscp:BDPT_JIT_FLAGS=-DBDPT_SCP=0" OUT=gpurun_out/s8_ab_scp_caustic8.txt bash scripts/ab.sh || exit 1
+  ARGS="--scene cornell --streams 64" ROUNDS=2 \
+    VARIANTS="units:BDPT_UNITS=8 units_fence:BDPT_UNITS=8;BDPT_JIT_FLAGS=-DBDPT_UNITS_FENCE=1" OUT=gpurun_out/s8_ab_fence.txt bash scripts/ab.sh || exit 1
+  timeout -k 10 500 python scripts/shard_probe.py --scene caustic --passes 128 --strong --reps 20 > gpurun_out/s8_caustic_strong.txt 2>&1 || { tail -20 gpurun_out/s8_caustic_strong.txt; exit 1; }
+  tail -8 gpurun_out/s8_caustic_strong.txt
+  for w in cornell1080 caustic8 weak64; do
+    timeout -k 10 400 python bench.py --workload $w > gpurun_out/s8_bench_$w.log 2>&1 || { tail -20 gpurun_out/s8_bench_$w.log; exit 1; }
+    grep '^{' gpurun_out/s8_bench_$w.log | tail -1 > gpurun_out/s8_bench_$w.json
+    python3 -c "import json; d=json.load(open('gpurun_out/s8_bench_$w.json')); print('$w', d['value'], d['ms_per_step'], d['roofline']['frac'], d['roofline'].get('traffic_over_model'), d.get('speedup_vs_cpu_node_estimate'))"
+  done
+}
+
+s9() {
+  # the final build (sin/cos planes off in the pool build): GPU suite, caustic8 bench, then
+  # per-workload rocprof stats + PMC records
+  pytest_gpu s9_pytest_gpu.log tests || exit 1
+  timeout -k 10 400 python bench.py --workload caustic8 > gpurun_out/s9_bench_caustic8.log 2>&1 || { tail -20 gpurun_out/s9_bench_caustic8.log; exit 1; }
+  grep '^{' gpurun_out/s9_bench_caustic8.log | tail -1 > gpurun_out/s9_bench_caustic8.json
+  python3 -c "import json; d=json.load(open('gpurun_out/s9_bench_caustic8.json')); print('caustic8', d['value'], d['ms_per_step'], d['roofline']['frac'])"
+  WORKLOADS="cornell1080:64:cornell1080:BDPT_UNITS=8 cornell1080:64:cornell1080s64:BDPT_UNITS=0 caustic8:128:caustic8:BDPT_POOL=16 weak64:32" \
+    bash scripts/profile_workloads.sh
+}
+
 "$@"
