@@ -640,22 +640,26 @@ def main():
         roofline = None
         if w is not None:
             samples_per_launch = own_pixels * passes_per_launch
+            # random-table bytes per sample: 4 B per value the path uses (WORK rng_reads, the
+            # oracle's count); kernels with the sin/cos planes load a segment's d_Rand[j..j+3] and
+            # two 8-B {sin, cos} pairs instead of d_Rand[j..j+4]: 32 B where 20 were
+            rng_bytes = 4 * w["rng_reads"] * (32 / 20 if "sincos_planes" in features else 1)
             if "unit_fold" in features:
                 # ordered in-kernel fold: colors + counter read and written once per unit of
                 # kUnitPasses (8) passes, pixels once per launch; no radiance buffer
                 per_unit = max(1.0, passes_per_launch / 8)          # units of a tile per launch
-                bytes_per_launch = own_pixels * (32 * per_unit + 4) + samples_per_launch * 4 * w["rng_reads"]
+                bytes_per_launch = own_pixels * (32 * per_unit + 4) + samples_per_launch * rng_bytes
             elif "pixel_pools" in features:
                 # pixel pools: the counter and a 16-B pass mask once per pixel; per sample the 12 B
                 # of radiance only when it is not +0 (WORK _nonzero: the oracle's fraction)
                 nz = w.get("_nonzero", 1.0)
-                bytes_per_launch = own_pixels * (4 + 16) + samples_per_launch * (4 * w["rng_reads"] + 12 * nz)
+                bytes_per_launch = own_pixels * (4 + 16) + samples_per_launch * (rng_bytes + 12 * nz)
             elif r.last_streams > 1:
                 # pass streams: the path kernel reads the counter once and writes 12 B of radiance
                 # per sample; the fold kernel (not this launch) does the colors/pixels RMW
-                bytes_per_launch = own_pixels * 4 + samples_per_launch * (4 * w["rng_reads"] + 12)
+                bytes_per_launch = own_pixels * 4 + samples_per_launch * (rng_bytes + 12)
             else:
-                bytes_per_launch = own_pixels * ACCUM_BYTES_PER_PIXEL + samples_per_launch * 4 * w["rng_reads"]
+                bytes_per_launch = own_pixels * ACCUM_BYTES_PER_PIXEL + samples_per_launch * rng_bytes
             gbs = bytes_per_launch / avg_launch_s / 1e9
             fl = flop_per_sample(w) * samples_per_launch / avg_launch_s / 1e12
             single = world == 1 and ndev == 1

@@ -22,7 +22,7 @@ DIFF, SPEC, REFR, LITE = 0, 1, 2, 3
 KEY_UP, KEY_DOWN, KEY_LEFT, KEY_RIGHT, KEY_PAGE_UP, KEY_PAGE_DOWN = range(0x101, 0x107)
 CHOICES = {1: "decided", 2: "fused", 4: "paired", 8: "quarter", 16: "pools", 32: "units"}   # BDPT_CHOICE_*
 FEATURES = {1: "specialized", 2: "det_skip", 4: "zero_exit", 8: "last_skip", 16: "bvh", 32: "pass_streams",
-            64: "pixel_pools", 128: "unit_fold"}
+            64: "pixel_pools", 128: "unit_fold", 256: "sincos_planes"}
 
 
 class Vec(ctypes.Structure):

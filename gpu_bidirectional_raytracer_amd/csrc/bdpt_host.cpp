@@ -1378,6 +1378,7 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
         c->last_specialized = jf != nullptr;
         c->last_features = BDPT_FEAT_LAST_SKIP | (bvh ? BDPT_FEAT_BVH : 0) | (st ? BDPT_FEAT_STREAMS : 0) |
                            (pooled ? BDPT_FEAT_POOLS : 0) | (unitsl ? BDPT_FEAT_UNITS : 0) |
+                           (st && !pooled ? BDPT_FEAT_SCP : 0) |
                            (jf ? BDPT_FEAT_SPECIALIZED | BDPT_FEAT_DET_SKIP | (c->jit_zero_exit ? BDPT_FEAT_ZERO_EXIT : 0) : 0);
         void* kargs[] = {&a};
         grid.z = a.streams;

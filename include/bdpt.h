@@ -173,6 +173,8 @@ int  bdpt_last_traversal(const bdpt_ctx *ctx);
 #define BDPT_FEAT_STREAMS    32             /* pass streams (one pass per lane + ordered fold)*/
 #define BDPT_FEAT_POOLS      64             /* pass streams with pixel pools (lanes restart on
                                                new pixels of their pass, claimed in chunks)   */
+#define BDPT_FEAT_SCP       256             /* sin/cos planes: the angles' sinf/cosf loaded, not
+                                               evaluated (pass streams / units, not pools)     */
 #define BDPT_FEAT_UNITS     128             /* pass streams with the ordered fold in the kernel:
                                                units of (tile, range of passes) in range order,
                                                running mean in registers, no radiance buffer   */
