@@ -129,4 +129,26 @@ s9() {
     bash scripts/profile_workloads.sh
 }
 
+s10() {
+  # the driver's other entry points on the final build: smoke(), multi-rank rehearsals (gloo,
+  # ranks sharing the GPU), an in-process two-device group on one GPU (peer copies)
+  timeout -k 10 300 python -c "import __graft_entry__ as e; e.smoke()" > gpurun_out/s10_smoke.log 2>&1 || { tail -20 gpurun_out/s10_smoke.log; exit 1; }
+  tail -1 gpurun_out/s10_smoke.log
+  NS="2 4" WORKLOADS="cornell1080 caustic8" STEPS_N=4 bash scripts/rehearse.sh || exit 1
+  for w in cornell1080 caustic8; do for n in 2 4; do grep '^{' gpurun_out/rehearse_${w}_$n.log | tail -1 > gpurun_out/s10_rehearse_${w}_$n.json; done; done
+  timeout -k 10 300 python bench.py --gpus 2 --devices 0,0 --steps 5 --no-cpu-baseline > gpurun_out/s10_inproc.log 2>&1 || { tail -20 gpurun_out/s10_inproc.log; exit 1; }
+  grep '^{' gpurun_out/s10_inproc.log | tail -1 > gpurun_out/s10_inproc.json
+  for f in gpurun_out/s10_rehearse_*.json gpurun_out/s10_inproc.json; do
+    python3 -c "
+import json; d=json.load(open('$f'))
+print('$f', d['n_gpus'], d['value'], d['reduce_backend'], 'modes_agree', d.get('modes_agree'), d.get('rccl_version'))"
+  done
+}
+
+s11() {
+  # pool kernel occupancy: 7 waves/SIMD (6 VGPRs spilled) against the default 6, caustic8 bench
+  MODE=bench ARGS="--workload caustic8 --no-cpu-baseline" ROUNDS=2 \
+    VARIANTS="w6: w7:BDPT_JIT_WAVES=7;BDPT_JIT_SCRATCH_OK=1" OUT=gpurun_out/s11_ab_waves.txt bash scripts/ab.sh || exit 1
+}
+
 "$@"
