@@ -336,9 +336,11 @@ extern "C" __global__ __launch_bounds__(256) void bdpt_rand_planar_kernel(const 
 }
 
 // {sinf, cosf}(2 pi u) for every entry u of the planar copy (BDPT_SCP): the path kernel's own
-// sincos_cr on the same float argument 2.f * kPi * u, with the same LDS table (bdpt_math.h), so
-// each stored pair is what the path kernel would compute for that entry.  7.7 M evaluations
-// per table, once per bdpt_generate_rand.
+// sincos_cr on the same float argument 2.f * kPi * u, with the 512-entry table (bdpt_math.h), so
+// each stored pair is what the path kernel would compute for that entry (a build with the
+// 256-entry BDPT_SC_COARSE table computes the same pair: both are the correctly rounded values,
+// checked for every float argument by tests/test_math.py).  7.7 M evaluations per table, once per
+// bdpt_generate_rand.
 extern "C" __global__ __launch_bounds__(256) void bdpt_sincos_planar_kernel(const float* __restrict__ rndp,
                                                                           float2* __restrict__ scp) {
     __shared__ double sct[BDPT_SC_N];
