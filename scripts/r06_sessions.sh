@@ -151,4 +151,17 @@ s11() {
     VARIANTS="w6: w7:BDPT_JIT_WAVES=7;BDPT_JIT_SCRATCH_OK=1" OUT=gpurun_out/s11_ab_waves.txt bash scripts/ab.sh || exit 1
 }
 
+s12() {
+  # other scenes on the final build (BVH scenes take the precompiled kernels with the sin/cos
+  # planes), and the default bench line with the round-6 PMC records
+  for sc in complex mod_cornell cornell_glass; do
+    timeout -k 10 400 python bench.py --scene $sc --no-cpu-baseline --steps 5 > gpurun_out/s12_bench_$sc.log 2>&1 || { tail -20 gpurun_out/s12_bench_$sc.log; exit 1; }
+    grep '^{' gpurun_out/s12_bench_$sc.log | tail -1 > gpurun_out/s12_bench_$sc.json
+    python3 -c "import json; d=json.load(open('gpurun_out/s12_bench_$sc.json')); print('$sc', d['value'], d['ms_per_step'], d['config']['traversal'], d['roofline'] and d['roofline']['kernel_features'])"
+  done
+  timeout -k 10 400 python bench.py > gpurun_out/s12_bench_default.log 2>&1 || { tail -20 gpurun_out/s12_bench_default.log; exit 1; }
+  grep '^{' gpurun_out/s12_bench_default.log | tail -1 > gpurun_out/s12_bench_default.json
+  python3 -c "import json; d=json.load(open('gpurun_out/s12_bench_default.json')); r=d['roofline']; print('default', d['value'], r['frac'], r['traffic'], r['traffic_over_model'], r.get('valu_busy_pmc'), d.get('speedup_vs_cpu_node_estimate'))"
+}
+
 "$@"
