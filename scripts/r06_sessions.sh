@@ -164,4 +164,13 @@ s12() {
   python3 -c "import json; d=json.load(open('gpurun_out/s12_bench_default.json')); r=d['roofline']; print('default', d['value'], r['frac'], r['traffic'], r['traffic_over_model'], r.get('valu_busy_pmc'), d.get('speedup_vs_cpu_node_estimate'))"
 }
 
+s13() {
+  # the sin/cos planes in the precompiled BVH kernels: this build against one with BDPT_SCP=0
+  # (make variant NAME=noscp EXTRA_HIPFLAGS=-DBDPT_SCP=0)
+  for sc in complex mod_cornell; do
+    MODE=bench ARGS="--scene $sc --no-cpu-baseline --steps 5" ROUNDS=2 \
+      VARIANTS="scp: noscp:BDPT_LIB=variants/noscp/libbdpt.so" OUT=gpurun_out/s13_ab_scp_bvh.txt bash scripts/ab.sh || exit 1
+  done
+}
+
 "$@"
