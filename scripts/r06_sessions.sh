@@ -173,4 +173,11 @@ s13() {
   done
 }
 
+s14() {
+  # the final tree: the GPU suite once more (the driver's round-end command) and smoke()
+  pytest_gpu s14_pytest_gpu.log tests || exit 1
+  timeout -k 10 300 python -c "import __graft_entry__ as e; e.smoke()" > gpurun_out/s14_smoke.log 2>&1 || { tail -20 gpurun_out/s14_smoke.log; exit 1; }
+  tail -1 gpurun_out/s14_smoke.log
+}
+
 "$@"
