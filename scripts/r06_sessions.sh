@@ -180,4 +180,10 @@ s14() {
   tail -1 gpurun_out/s14_smoke.log
 }
 
+s15() {
+  # do transcendental / fp64 instructions take fp32 VALU issue cycles? (scripts/valu_overlap.hip)
+  timeout -k 10 120 ./scripts/valu_overlap > gpurun_out/s15_valu_overlap.txt 2>&1 || { tail -5 gpurun_out/s15_valu_overlap.txt; exit 1; }
+  cat gpurun_out/s15_valu_overlap.txt
+}
+
 "$@"
