@@ -246,6 +246,9 @@ __device__ __forceinline__ f3 cosine_tail(f3 w, f3 u, float u_phi, float u_r2, f
 #ifndef BDPT_SCP
 #define BDPT_SCP 1
 #endif
+#ifndef BDPT_SCP_LATE
+#define BDPT_SCP_LATE 0
+#endif
 
 // Fused S = 1 kernel: a lane whose path ends parks until at least BDPT_REGEN_K lanes of its wave
 // (or all of its live lanes) are parked; then they start their next passes together, so the
@@ -528,6 +531,29 @@ __device__ __forceinline__ void load_rand_scp(__amdgpu_buffer_rsrc_t rs, __amdgp
     q1 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, vo, P4, 0));
     q2 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, vo, 2 * P4, 0));
     q3 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, vo, 3 * P4, 0));
+    const u2v a = __builtin_amdgcn_raw_buffer_load_b64(rsc, vs, 0, 0);
+    const u2v b = __builtin_amdgcn_raw_buffer_load_b64(rsc, vs, 4 * P8, 0);
+    s0 = __uint_as_float(a.x); c0 = __uint_as_float(a.y);
+    s4 = __uint_as_float(b.x); c4 = __uint_as_float(b.y);
+}
+
+// the two parts of load_rand_scp on their own (BDPT_SCP_LATE)
+__device__ __forceinline__ void load_rand4p(__amdgpu_buffer_rsrc_t rs, unsigned j, float& q0, float& q1,
+                                            float& q2, float& q3) {
+    const unsigned qd = j / 25u, r = j - qd * 25u;
+    const unsigned vo = (r * BDPT_DEV_RANDP_PL + qd) * 4u;
+    constexpr unsigned P4 = BDPT_DEV_RANDP_PL * 4u;
+    q0 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, vo, 0, 0));
+    q1 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, vo, P4, 0));
+    q2 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, vo, 2 * P4, 0));
+    q3 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, vo, 3 * P4, 0));
+}
+__device__ __forceinline__ void load_sc(__amdgpu_buffer_rsrc_t rsc, unsigned j, float& s0, float& c0,
+                                        float& s4, float& c4) {
+    typedef unsigned u2v __attribute__((ext_vector_type(2)));
+    const unsigned qd = j / 25u, r = j - qd * 25u;
+    const unsigned vs = (r * BDPT_DEV_RANDP_PL + qd) * 8u;
+    constexpr unsigned P8 = BDPT_DEV_RANDP_PL * 8u;
     const u2v a = __builtin_amdgcn_raw_buffer_load_b64(rsc, vs, 0, 0);
     const u2v b = __builtin_amdgcn_raw_buffer_load_b64(rsc, vs, 4 * P8, 0);
     s0 = __uint_as_float(a.x); c0 = __uint_as_float(a.y);
@@ -1023,8 +1049,11 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
     float sn0 = 0.f, cs0 = 0.f, sn4 = 0.f, cs4 = 0.f;
     const __amdgpu_buffer_rsrc_t rss = __builtin_amdgcn_make_buffer_rsrc(
         (void*)a.scp, (short)0, (int)(BDPT_DEV_RANDP_PLANES * BDPT_DEV_RANDP_PL * 8u), 0x00020000);
+    // BDPT_SCP_LATE (experiment): the pairs loaded at the top of their own segment instead of
+    // one segment ahead with d_Rand[j..j+3] (shorter register lifetimes, less time to arrive)
     auto load_plan = [&](unsigned jj) {
-        if constexpr (kScp) load_rand_scp(rsp, rss, jj, q0, q1, q2, q3, sn0, cs0, sn4, cs4);
+        if constexpr (kScp && BDPT_SCP_LATE) load_rand4p(rsp, jj, q0, q1, q2, q3);
+        else if constexpr (kScp) load_rand_scp(rsp, rss, jj, q0, q1, q2, q3, sn0, cs0, sn4, cs4);
         else load_rand5p(rsp, jj, q0, q1, q2, q3, q4);
     };
     if (planar) load_plan(j);
@@ -1061,6 +1090,9 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
         bool done = false, diff = false;
         float t = 1e20f;
         int id = -1;
+        if constexpr (kScp && BDPT_SCP_LATE) {
+            if (alive) load_sc(rss, j, sn0, cs0, sn4, cs4);
+        }
         if (alive) {
             if (fresh) {                  // camera ray (:562-600); d_Rand[kk] == q0 (kk == j)
                 const float4 c0 = K[0], c1 = K[1], c2 = K[2], c3 = K[3], k4 = K[4];

@@ -186,4 +186,14 @@ s15() {
   cat gpurun_out/s15_valu_overlap.txt
 }
 
+s16() {
+  # the sin/cos pairs loaded at the top of their own segment (BDPT_SCP_LATE) against one segment
+  # ahead (default) and no planes
+  for w in cornell1080 weak64; do
+    MODE=bench ARGS="--workload $w --no-cpu-baseline" ROUNDS=2 \
+      VARIANTS="early: late:BDPT_JIT_FLAGS=-DBDPT_SCP_LATE=1 noscp:BDPT_JIT_FLAGS=-DBDPT_SCP=0" \
+      OUT=gpurun_out/s16_ab_scp_late.txt bash scripts/ab.sh || exit 1
+  done
+}
+
 "$@"
