@@ -196,4 +196,10 @@ s16() {
   done
 }
 
+s17() {
+  # the 1080p whole-frame mode test, now against the oracle over every pixel
+  pytest_gpu s17_pytest_wholeframe.log tests/test_gpu_configs.py -k whole_frame --durations=5 || exit 1
+  grep -A8 "slowest" gpurun_out/s17_pytest_wholeframe.log
+}
+
 "$@"

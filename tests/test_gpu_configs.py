@@ -191,10 +191,11 @@ def test_1080p_whole_frame_identical_in_every_kernel_mode(gpu, rnd0, name, monke
     """Whole 1921x1081 frames (not sampled rows): the same 128 passes rendered by every kernel
     mode -- the ordered in-kernel fold (units), pixel pools with the sample lists, two and one
     pass(es) per lane with the separate fold, and the fused S = 1 kernel -- are bit-identical over
-    every pixel, and rows spread over the frame equal the oracle.  The modes share the sphere
-    tests and shading but differ in everything that maps pixels and passes to lanes, stores
-    radiance and folds it; a band-local defect in one of them cannot hide between sampled rows
-    (VERDICT r5 weak item 8)."""
+    every pixel, and the whole frame equals the oracle bit for bit (266 M samples: ~15 s of the
+    OpenMP oracle on cornell at 16 threads, a few on caustic).  The modes share the sphere tests
+    and shading but differ in everything that maps pixels and passes to lanes, stores radiance and
+    folds it; a band-local defect in one of them cannot hide between sampled rows (VERDICT r5 weak
+    item 8)."""
     W, H, n = 1921, 1081, 128
     sid, vlp = _schedule(n)
     modes = [("units", 128, {"BDPT_UNITS": "8", "BDPT_POOL": "0"}, "unit_fold"),
@@ -219,6 +220,6 @@ def test_1080p_whole_frame_identical_in_every_kernel_mode(gpu, rnd0, name, monke
         _same(col, ref_col, f"{tag} vs units: colors")
         _same(cnt, ref_cnt, f"{tag} vs units: counter")
     lp = oracle.light_pass(sp, rnd0, 0)
-    for y in (0, 137, 540, 811, H - 1):
-        ocol, ocnt, _ = oracle.path_passes(sp, rnd0, cam, W, H, lp, sid, vlp, rows=(y, y + 1))
-        _same(ref_col[y], ocol[y], f"row {y}")
+    ocol, ocnt, _ = oracle.path_passes(sp, rnd0, cam, W, H, lp, sid, vlp)
+    _same(ref_col, ocol, "whole frame vs oracle: colors")
+    _same(ref_cnt, ocnt, "whole frame vs oracle: counter")
