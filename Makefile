@@ -55,8 +55,18 @@ $(LIB): $(BUILD)/bdpt_kernels.o $(BUILD)/bdpt_host.o $(BUILD)/bdpt_bvh.o $(BUILD
 	mkdir -p $(dir $(LIB))
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lm -ldl
 
-$(HOST): $(CSRC)/smallpt.c include/bdpt.h $(LIB)
+$(HOST): $(CSRC)/smallpt.c $(CSRC)/smallpt_app.h include/bdpt.h $(LIB)
 	$(CC) $(CFLAGS) -o $@ $< -L$(PKG) -lbdpt -lm -Wl,-rpath,'$$ORIGIN'
+
+# the optional display: X11 + GLX viewer over HIP-GL interop; built when the
+# image has the GL/X11 headers (libbdpt itself never links OpenGL)
+GLHOST   := $(PKG)/smallpt_gl
+GL_OK    := $(shell test -f /usr/include/GL/glx.h -a -f /usr/include/X11/Xlib.h && echo 1)
+ifeq ($(GL_OK),1)
+all: $(GLHOST)
+endif
+$(GLHOST): $(CSRC)/smallpt_gl.c $(CSRC)/smallpt_app.h include/bdpt.h $(LIB)
+	$(CC) $(CFLAGS) -o $@ $< -L$(PKG) -lbdpt -lGL -lX11 -lm -Wl,-rpath,'$$ORIGIN'
 
 $(ORACLE): oracle/bdpt_oracle.c include/bdpt.h
 	$(CC) -O2 -std=gnu11 -fPIC -shared -fopenmp -ffp-contract=off -Wall -o $@ $< -lm

@@ -414,6 +414,18 @@ class Renderer:
         self._chk(lib.bdpt_device_buffers(self._h, ctypes.byref(c), ctypes.byref(n), ctypes.byref(p)))
         return c.value, n.value, p.value
 
+    # -- optional display: HIP-GL interop of the caller's pixel-unpack buffer
+    def gl_register_pbo(self, pbo: int) -> None:
+        """cudaGLRegisterBufferObject (smallpt_cpu.c:122): needs a current OpenGL context."""
+        self._chk(lib.bdpt_gl_register_pbo(self._h, int(pbo)))
+
+    def gl_publish(self) -> None:
+        """IdleFunc's map / render / unmap (display_func.c:199-215): the frame's pixels into the PBO."""
+        self._chk(lib.bdpt_gl_publish(self._h))
+
+    def gl_unregister(self) -> None:
+        self._chk(lib.bdpt_gl_unregister(self._h))
+
 
 # ---- the reference's operator interface (smallpt_cpu.c / display_func.c) --------------------
 

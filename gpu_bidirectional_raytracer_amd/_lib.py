@@ -113,6 +113,9 @@ _SIGS = [
     ("bdpt_get_scene", ctypes.c_int, [_P, ctypes.POINTER(Sphere), ctypes.c_uint]),
     ("bdpt_device_buffers", ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.POINTER(_P), ctypes.POINTER(_P)]),
     ("bdpt_update_pixels", ctypes.c_int, [_P]),
+    ("bdpt_gl_register_pbo", ctypes.c_int, [_P, ctypes.c_uint]),
+    ("bdpt_gl_publish", ctypes.c_int, [_P]),
+    ("bdpt_gl_unregister", ctypes.c_int, [_P]),
     ("bdpt_write_radiance", ctypes.c_int, [_P, _P, _P]),
     ("bdpt_save_checkpoint", ctypes.c_int, [_P, ctypes.c_char_p, _P, ctypes.c_uint]),
     ("bdpt_load_checkpoint", ctypes.c_int, [_P, ctypes.c_char_p, _P, ctypes.c_uint]),

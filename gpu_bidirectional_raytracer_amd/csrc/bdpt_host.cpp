@@ -8,6 +8,7 @@
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
+#include <hip/hip_gl_interop.h>         // hipGraphicsGLRegisterBuffer (the optional display, 8(f)4)
 #include <rccl/rccl.h>                 // types and prototypes only: librccl is opened with dlopen
 #include <math.h>
 #include <stdarg.h>
@@ -207,6 +208,8 @@ struct bdpt_ctx {
     unsigned* d_ftmpc = nullptr;
     char reduce_note[256] = {0};        // the RCCL version and communicator, or why RCCL is not used
     bdpt_cpu_ctx* cpu = nullptr;        // device == BDPT_DEVICE_CPU: the host backend (bdpt_cpu.cpp)
+    hipGraphicsResource_t gl_res = nullptr;   // registered GL pixel-unpack buffer (bdpt_gl_register_pbo)
+    unsigned gl_pbo = 0;
 };
 enum { kReduceNone = 0, kReduceRccl = 1, kReducePeer = 2 };
 
@@ -897,6 +900,7 @@ void bdpt_destroy(bdpt_ctx* c) {
         }
         (void)hipFree(c->d_prof);
     }
+    if (c->gl_res) (void)hipGraphicsUnregisterResource(c->gl_res);
     release(c);
     delete c;
 }
@@ -2169,6 +2173,85 @@ int bdpt_write_radiance(bdpt_ctx* c, const bdpt_vec* colors, const unsigned* cou
     if (!c || !colors || !counter) return BDPT_EINVAL;
     if (int rc = one_write_radiance(c, colors, counter, c->multi)) return rc;
     return forward(c, [&](bdpt_ctx* p) { return one_write_radiance(p, colors, counter, true); });
+}
+
+// ---- optional display: HIP-GL interop of the window's pixel-unpack buffer ----
+// The reference registers its PBO once (cudaGLRegisterBufferObject, smallpt_cpu.c:112-123) and per
+// frame maps it, lets the path kernel write pixels_buf = the mapped pointer, and unmaps it
+// (IdleFunc, display_func.c:199-215).  Here the kernels keep writing d_pixels (the read-back,
+// checkpoint and multi-device paths all read it) and a publish copies the finished frame into the
+// mapped buffer on the context's stream: one 4*W*H-byte device copy per displayed frame (8.3 MB
+// at 1080p, ~2 us of HBM time), the same bytes in the same bottom-row-first order.
+//
+// hipGraphicsGLRegisterBuffer needs an OpenGL context current on the calling thread; without one
+// it is undefined what the runtime does, so the context is looked up first (GLX, then EGL) in
+// libraries the process has already loaded -- libbdpt itself never links or loads OpenGL.
+static bool gl_context_current() {
+    typedef void* (*cur_fn)(void);
+    const char* const libs[2] = {"libGL.so.1", "libEGL.so.1"};
+    const char* const syms[2] = {"glXGetCurrentContext", "eglGetCurrentContext"};
+    for (int k = 0; k < 2; k++) {
+        cur_fn f = (cur_fn)dlsym(RTLD_DEFAULT, syms[k]);
+        void* h = nullptr;
+        if (!f && (h = dlopen(libs[k], RTLD_LAZY | RTLD_NOLOAD)) != nullptr) f = (cur_fn)dlsym(h, syms[k]);
+        const bool cur = f && f() != nullptr;
+        if (h) dlclose(h);
+        if (cur) return true;
+    }
+    return false;
+}
+
+int bdpt_gl_register_pbo(bdpt_ctx* c, unsigned pbo) {
+    if (!c) return BDPT_EINVAL;
+    if (c->cpu) return fail(c, BDPT_EINVAL, "bdpt_gl_register_pbo: the CPU backend has no device pixels");
+    if (!pbo) return fail(c, BDPT_EINVAL, "bdpt_gl_register_pbo: buffer name 0");
+    if (!gl_context_current())
+        return fail(c, BDPT_EINVAL, "bdpt_gl_register_pbo: no OpenGL context is current on this thread");
+    HIPCHK(c, hipSetDevice(c->device));
+    if (c->gl_res) {
+        HIPCHK(c, hipGraphicsUnregisterResource(c->gl_res));
+        c->gl_res = nullptr;
+        c->gl_pbo = 0;
+    }
+    HIPCHK(c, hipGraphicsGLRegisterBuffer(&c->gl_res, pbo, hipGraphicsRegisterFlagsWriteDiscard));
+    c->gl_pbo = pbo;
+    return BDPT_OK;
+}
+
+int bdpt_gl_publish(bdpt_ctx* c) {
+    if (!c) return BDPT_EINVAL;
+    if (!c->gl_res) return fail(c, BDPT_ESTATE, "bdpt_gl_publish: no buffer registered (bdpt_gl_register_pbo)");
+    void* pix = nullptr;
+    if (int rc = bdpt_device_buffers(c, nullptr, nullptr, &pix)) return rc;   // multi: the assembled frame
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipGraphicsMapResources(1, &c->gl_res, c->stream));
+    // from here the buffer is mapped: every path below unmaps it before returning
+    const size_t bytes = 4 * (size_t)c->W * c->H;
+    void* dst = nullptr;
+    size_t size = 0;
+    hipError_t e = hipGraphicsResourceGetMappedPointer(&dst, &size, c->gl_res);
+    bool small = false;
+    if (e == hipSuccess && size < bytes) small = true;
+    else if (e == hipSuccess) e = hipMemcpyAsync(dst, pix, bytes, hipMemcpyDeviceToDevice, c->stream);
+    const hipError_t u = hipGraphicsUnmapResources(1, &c->gl_res, c->stream);
+    if (small)
+        return fail(c, BDPT_EINVAL, "bdpt_gl_publish: buffer %u holds %zu bytes, the frame needs %zu",
+                    c->gl_pbo, size, bytes);
+    if (e != hipSuccess) return fail(c, BDPT_EHIP, "bdpt_gl_publish: mapped copy: %s", hipGetErrorString(e));
+    if (u != hipSuccess) return fail(c, BDPT_EHIP, "bdpt_gl_publish: unmap: %s", hipGetErrorString(u));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return BDPT_OK;
+}
+
+int bdpt_gl_unregister(bdpt_ctx* c) {
+    if (!c) return BDPT_EINVAL;
+    if (!c->gl_res) return BDPT_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    hipGraphicsResource_t r = c->gl_res;
+    c->gl_res = nullptr;
+    c->gl_pbo = 0;
+    HIPCHK(c, hipGraphicsUnregisterResource(r));
+    return BDPT_OK;
 }
 
 // bdpt_save_checkpoint / bdpt_load_checkpoint: bdpt_ckpt.c (over the entry points above)

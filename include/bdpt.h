@@ -242,6 +242,22 @@ int  bdpt_device_buffers(bdpt_ctx *ctx, void **colors, void **counter, void **pi
 /* Recompute pixels (toInt gamma) from colors on the device, e.g. after a cross-GPU reduce. */
 int  bdpt_update_pixels(bdpt_ctx *ctx);
 
+/* ---- optional display: HIP-GL interop ----
+ * The caller owns the window, its OpenGL context (current on the calling thread) and a
+ * pixel-unpack buffer of at least 4*W*H bytes (glGenBuffers + glBufferData(GL_PIXEL_UNPACK_BUFFER,
+ * 4*W*H, NULL, GL_DYNAMIC_COPY), as CreatePBO smallpt_cpu.c:112-123 makes it).
+ * bdpt_gl_register_pbo replaces cudaGLRegisterBufferObject (smallpt_cpu.c:122): BDPT_EINVAL when
+ * no GL context is current (GLX or EGL, looked up in the libraries the process has loaded) or on
+ * the CPU backend.  bdpt_gl_publish replaces IdleFunc's map / UpdateRendering / unmap bracket
+ * (display_func.c:199-215): it maps the buffer, copies the frame's 8-bit pixels into it (the
+ * layout of bdpt_read_pixels: RGBA, bottom row first, as glTexSubImage2D takes it; for a
+ * multi-device context the assembled frame), unmaps it -- on every path -- and synchronises;
+ * BDPT_ESTATE before a register, BDPT_EINVAL when the buffer is smaller than the frame.
+ * bdpt_gl_unregister (also done by bdpt_destroy) must run while the GL context still exists. */
+int  bdpt_gl_register_pbo(bdpt_ctx *ctx, unsigned int pbo);
+int  bdpt_gl_publish(bdpt_ctx *ctx);
+int  bdpt_gl_unregister(bdpt_ctx *ctx);
+
 /* ---- checkpoint / resume of the accumulation (no reference counterpart: the reference keeps
  * it only in dev_colors/dev_counter) ---- */
 /* Upload colors/counter (W*H each; the counterpart of bdpt_read_radiance); pixels are

@@ -202,4 +202,9 @@ s17() {
   grep -A8 "slowest" gpurun_out/s17_pytest_wholeframe.log
 }
 
+s18() {
+  # the display entry points on the GPU (no GL context on the node: refusal + bit-exact render after)
+  pytest_gpu s18_pytest_display.log tests/test_display.py tests/test_gpu_parity.py || exit 1
+}
+
 "$@"
