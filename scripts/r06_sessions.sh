@@ -207,4 +207,11 @@ s18() {
   pytest_gpu s18_pytest_display.log tests/test_display.py tests/test_gpu_parity.py || exit 1
 }
 
+s19() {
+  # configs[3] against the oracle over the whole frame at 4096 spp; the whole-frame mode test with
+  # cornell_glass added
+  pytest_gpu s19_pytest_configs.log tests/test_gpu_configs.py --durations=10 || exit 1
+  grep -A12 "slowest" gpurun_out/s19_pytest_configs.log
+}
+
 "$@"
