@@ -214,4 +214,14 @@ s19() {
   grep -A12 "slowest" gpurun_out/s19_pytest_configs.log
 }
 
+s20() {
+  # the final tree (display entry points, whole-frame config tests): GPU suite, smoke, default bench
+  pytest_gpu s20_pytest_gpu.log tests || exit 1
+  timeout -k 10 300 python -c "import __graft_entry__ as e; e.smoke()" > gpurun_out/s20_smoke.log 2>&1 || { tail -20 gpurun_out/s20_smoke.log; exit 1; }
+  tail -1 gpurun_out/s20_smoke.log
+  timeout -k 10 400 python bench.py > gpurun_out/s20_bench_default.log 2>&1 || { tail -20 gpurun_out/s20_bench_default.log; exit 1; }
+  grep '^{' gpurun_out/s20_bench_default.log | tail -1 > gpurun_out/s20_bench_default.json
+  python3 -c "import json; d=json.load(open('gpurun_out/s20_bench_default.json')); r=d['roofline']; print('default', d['value'], d['ms_per_step'], r['frac'], r['avg_launch_ms'], d.get('speedup_vs_cpu_node_estimate'))"
+}
+
 "$@"
