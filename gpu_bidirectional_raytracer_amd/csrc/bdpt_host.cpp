@@ -2213,7 +2213,9 @@ int bdpt_gl_register_pbo(bdpt_ctx* c, unsigned pbo) {
         c->gl_res = nullptr;
         c->gl_pbo = 0;
     }
-    HIPCHK(c, hipGraphicsGLRegisterBuffer(&c->gl_res, pbo, hipGraphicsRegisterFlagsWriteDiscard));
+    hipGraphicsResource_t res = nullptr;                        // kept only on success
+    HIPCHK(c, hipGraphicsGLRegisterBuffer(&res, pbo, hipGraphicsRegisterFlagsWriteDiscard));
+    c->gl_res = res;
     c->gl_pbo = pbo;
     return BDPT_OK;
 }
