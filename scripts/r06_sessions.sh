@@ -224,4 +224,9 @@ s20() {
   python3 -c "import json; d=json.load(open('gpurun_out/s20_bench_default.json')); r=d['roofline']; print('default', d['value'], d['ms_per_step'], r['frac'], r['avg_launch_ms'], d.get('speedup_vs_cpu_node_estimate'))"
 }
 
+s21() {
+  # every reference scene on the final build (bench.py, 1921x1081, 32 passes per step)
+  timeout -k 10 1000 bash scripts/scenes_sweep.sh || exit 1
+}
+
 "$@"
