@@ -249,6 +249,12 @@ __device__ __forceinline__ f3 cosine_tail(f3 w, f3 u, float u_phi, float u_r2, f
 #ifndef BDPT_SCP_LATE
 #define BDPT_SCP_LATE 0
 #endif
+// Shadow rounds whose rays are all VLP rays (IntersectPVacuumDevice, device.cu:141-154, ignores
+// emitters) skip the emitters' sphere tests: the NEE rays fill the queue first, so a segment's
+// second round is usually VLP rays only.
+#ifndef BDPT_VAC_SKIP
+#define BDPT_VAC_SKIP 1
+#endif
 
 // Fused S = 1 kernel: a lane whose path ends parks until at least BDPT_REGEN_K lanes of its wave
 // (or all of its live lanes) are parked; then they start their next passes together, so the
@@ -1477,6 +1483,9 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
 #endif
                         BDPT_CNTN(7, 1);
                         auto step = [&](int s) -> bool {                  // IntersectP(Vacuum)Device
+                            // a round of VLP rays only (the queue holds the NEE rays first):
+                            // IntersectPVacuumDevice never counts an emitter, so its test is skipped
+                            if (BDPT_VAC_SKIP && emissive(s) && vacm == live) return true;
                             BDPT_CNTN(9, 1);
                             const tdet qd = sphere_det(geom(s), o, d);
                             if (small_sphere(s) && __builtin_amdgcn_ballot_w64(!(qd.det < 0.f)) == 0) {

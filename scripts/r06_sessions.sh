@@ -229,4 +229,14 @@ s21() {
   timeout -k 10 1000 bash scripts/scenes_sweep.sh || exit 1
 }
 
+s22() {
+  # emitter tests skipped in VLP-only shadow rounds (BDPT_VAC_SKIP): parity first, then A/B
+  pytest_gpu s22_pytest_parity.log tests/test_gpu_parity.py tests/test_gpu_fuzz.py || exit 1
+  for w in cornell1080 weak64 caustic8; do
+    MODE=bench ARGS="--workload $w --no-cpu-baseline" ROUNDS=2 \
+      VARIANTS="skip: noskip:BDPT_JIT_FLAGS=-DBDPT_VAC_SKIP=0" \
+      OUT=gpurun_out/s22_ab_vac_skip.txt bash scripts/ab.sh || exit 1
+  done
+}
+
 "$@"
