@@ -60,6 +60,8 @@ struct bdpt_path_args {
     const int* lights;              // indices of emitters (e != 0), ascending
     const float4* lightrec;         // per emitter: {p, rad}, {e, (4*pi*rad)*rad}
     const float4* geom;             // per sphere {p, rad*rad} (SGPR-resident traversal)
+    const float4* vgeom;            // the non-emitters' {p, rad*rad}, ascending index (n_vac of them):
+    int n_vac;                      // the sphere list of a VLP-only shadow round
     unsigned emis_mask;             // bit s = sphere s is emissive (sphere counts <= 32)
     const float* rnd;
     const float* rndp;              // the planar copy (BDPT_DEV_RANDP_*), pass-stream kernels

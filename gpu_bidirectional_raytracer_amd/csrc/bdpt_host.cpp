@@ -166,7 +166,8 @@ struct bdpt_ctx {
     bdpt_dev_sphere* d_sph = nullptr;
     unsigned sph_cap = 0;
     int* d_lights = nullptr;
-    float4* d_geom = nullptr;           // per sphere {p, rad^2}
+    float4* d_geom = nullptr;           // per sphere {p, rad^2}; then the n_vac non-emitters' (VLP-only shadow rounds)
+    unsigned n_vac = 0;
     float4* d_lightrec = nullptr;       // per emitter {p, rad}, {e, (4*pi*rad)*rad}
     unsigned emis_mask = 0;
     bdpt_dev_vec* d_colors = nullptr;
@@ -242,6 +243,7 @@ static int upload_scene(bdpt_ctx* c) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
     std::vector<bdpt_dev_sphere> ds(n);
     std::vector<float4> geom(n), lrec;
+    std::vector<float4> vgeom;                      // the non-emitters' geometry, ascending index
     c->lights.clear();
     c->emis_mask = 0;
     for (unsigned i = 0; i < n; i++) {
@@ -254,6 +256,7 @@ static int upload_scene(bdpt_ctx* c) {
         d.cx = s.c.x; d.cy = s.c.y; d.cz = s.c.z;
         d.refl = s.refl;
         geom[i] = make_float4(d.px, d.py, d.pz, d.rr);
+        if (s.e.x == 0.f && s.e.y == 0.f && s.e.z == 0.f) vgeom.push_back(geom[i]);
         if (!(s.e.x == 0.f && s.e.y == 0.f && s.e.z == 0.f)) {
             c->lights.push_back((int)i);
             if (i < 32) c->emis_mask |= 1u << i;
@@ -270,11 +273,15 @@ static int upload_scene(bdpt_ctx* c) {
         c->d_sph = nullptr; c->d_lights = nullptr; c->d_geom = nullptr; c->d_lightrec = nullptr;
         HIPCHK(c, hipMalloc(&c->d_sph, sizeof(bdpt_dev_sphere) * n));
         HIPCHK(c, hipMalloc(&c->d_lights, sizeof(int) * n));
-        HIPCHK(c, hipMalloc(&c->d_geom, sizeof(float4) * n));
+        HIPCHK(c, hipMalloc(&c->d_geom, 2 * sizeof(float4) * n));   // [n) by index, then the non-emitters
         HIPCHK(c, hipMalloc(&c->d_lightrec, 2 * sizeof(float4) * n));
         c->sph_cap = n;
     }
     if (n) HIPCHK(c, hipMemcpyAsync(c->d_geom, geom.data(), sizeof(float4) * n, hipMemcpyHostToDevice, c->stream));
+    c->n_vac = (unsigned)vgeom.size();
+    if (c->n_vac)
+        HIPCHK(c, hipMemcpyAsync(c->d_geom + n, vgeom.data(), sizeof(float4) * c->n_vac, hipMemcpyHostToDevice,
+                                 c->stream));
     if (!lrec.empty())
         HIPCHK(c, hipMemcpyAsync(c->d_lightrec, lrec.data(), sizeof(float4) * lrec.size(),
                                  hipMemcpyHostToDevice, c->stream));
@@ -648,6 +655,14 @@ static hipFunction_t jit_path_kernel_build(bdpt_ctx* c, bool streams, bool pair,
         if (!streams && !pair) all.push_back("-DBDPT_RNG_PAIR=0");
         if (streams && pool) all.push_back("-DBDPT_POOL=1");
         if (streams && units) all.push_back("-DBDPT_UNITS=1");
+        // VLP-only part-full shadow rounds over the non-emitters' list (BDPT_VAC_LIST): only where
+        // dropping the emitters saves a lane-group iteration (cornell: 8 of 9 spheres fit 4, 2, 1
+        // iterations instead of 5, 3, 2); elsewhere the staging costs (synthetic64 -0.4 %,
+        // profiles/r06_s24_ab_vac_list.txt)
+        bool vac_list = false;
+        for (unsigned k = 1; k <= 3; k++)
+            if ((1u << k) <= c->n_vac && (c->n_vac + (1u << k) - 1) >> k < (n + (1u << k) - 1) >> k) vac_list = true;
+        if (!vac_list) all.push_back("-DBDPT_VAC_LIST=0");
         if (const char* extra = getenv("BDPT_JIT_FLAGS")) {    // experiments: extra -D options
             std::string tok;
             for (const char* q = extra;; q++) {
@@ -671,7 +686,7 @@ static hipFunction_t jit_path_kernel_build(bdpt_ctx* c, bool streams, bool pair,
         if (!coarse && !user_coarse &&
             hipFuncGetAttribute(&stat, HIP_FUNC_ATTRIBUTE_SHARED_SIZE_BYTES, fn) == hipSuccess) {
             const size_t slots = units ? (size_t)std::max(units_env(), 16) : streams ? 1 : (size_t)fused_max_passes();
-            const size_t dyn = sizeof(float4) * (4 * (size_t)n + 3 * slots + 5 + 4 * 128 * 2) + sizeof(unsigned) * slots;
+            const size_t dyn = sizeof(float4) * (5 * (size_t)n + 3 * slots + 5 + 4 * 128 * 2) + sizeof(unsigned) * slots;
             const size_t lds = 160 * 1024, fine = lds / (dyn + stat), half = lds / (dyn + stat - 2048);
             if (fine < (size_t)waves && half > fine) {
                 coarse = true;
@@ -1110,6 +1125,8 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
     a.lights = c->d_lights;
     a.lightrec = c->d_lightrec;
     a.geom = c->d_geom;
+    a.vgeom = c->d_geom + c->spheres.size();
+    a.n_vac = (int)c->n_vac;
     a.emis_mask = c->emis_mask;
     a.rnd = c->d_rand;
     a.rndp = c->d_rndp;
@@ -1361,7 +1378,7 @@ static int one_path_passes(bdpt_ctx* c, const unsigned* sid, const int* vlp, int
 #else
         const size_t tree = 0, tree_ids = 0;                 // tree read through L1/L2
 #endif
-        const size_t tab = bvh ? tree + a.big_n : 4 * (size_t)a.n;
+        const size_t tab = bvh ? tree + a.big_n : 4 * (size_t)a.n + (size_t)a.n_vac;   // (bdpt_kernels.hip ntab)
         const size_t ids = bvh ? tree_ids + a.big_n : 0;
         // S per launch: a short last chunk gets no idle stream slices
         const bool st = (S < a.npass ? S : a.npass) > 1;     // the pass-stream kernel

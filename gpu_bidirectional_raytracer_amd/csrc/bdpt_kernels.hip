@@ -255,6 +255,17 @@ __device__ __forceinline__ f3 cosine_tail(f3 w, f3 u, float u_phi, float u_r2, f
 #ifndef BDPT_VAC_SKIP
 #define BDPT_VAC_SKIP 1
 #endif
+// The same rounds when they are part-full (<= 32 rays, traced by lane groups that split the sphere
+// list): the groups split the non-emitters' list (bdpt_path_args.vgeom, staged in LDS as GV).
+// Not in the pixel-pool build: caustic8 ran 2 % slower with it (profiles/r06_s23_ab_vac_list.txt);
+// scene-specialised builds only (the precompiled per-N instances would spill SGPRs from N = 9).
+#ifndef BDPT_VAC_LIST
+#ifdef BDPT_JIT
+#define BDPT_VAC_LIST 1
+#else
+#define BDPT_VAC_LIST 0
+#endif
+#endif
 
 // Fused S = 1 kernel: a lane whose path ends parks until at least BDPT_REGEN_K lanes of its wave
 // (or all of its live lanes) are parked; then they start their next passes together, so the
@@ -702,7 +713,7 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
     constexpr int kUnroll = N > 0 ? N : 1;
     constexpr bool kTreeLds = false;  // tree read through L1/L2: 4 workgroups per CU (+10 %)
     const int ntree = kTreeLds ? 2 * a.bvh_nn + a.bvh_ns : 0;
-    const int ntab = kBVH ? ntree + a.big_n : 4 * n;
+    const int ntab = kBVH ? ntree + a.big_n : 4 * n + a.n_vac;      // (bdpt_host.cpp tab)
     // pass stream: this workgroup's lanes render passes s0, s0+S, s0+2S, ... (slots k = 0, 1, ...)
     // of their pixels (S == 1: all, and each lane keeps the running mean itself; S > 1: radiance
     // goes to rbuf, bdpt_accum_kernel folds it in pass order).  Only the slots' VLPs and sids are
@@ -757,6 +768,7 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
     float4* E = smem + n;             // {ex, ey, ez, rad}
     float4* P = smem + 2 * n;         // {px, py, pz, 0}  (hit normal)
     float4* G = smem + 3 * n;         // {px, py, pz, rad^2}  (N == 0 traversal)
+    float4* GV = smem + 4 * n;        // the same for the non-emitters only (VLP-only shadow rounds)
     float4* ND = smem;                // BVH: nodes (2 float4 each)
     float4* SG = ND + 2 * a.bvh_nn;   // BVH: sphere geometry in leaf order
     float4* BG = smem + ntree;        // BVH: brute-force (wall) geometry
@@ -793,6 +805,8 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
             P[s] = make_float4(S.px, S.py, S.pz, 0.f);
             G[s] = make_float4(S.px, S.py, S.pz, S.rr);
         }
+        if constexpr (BDPT_VAC_LIST && !kPool)
+            for (int s = threadIdx.x; s < a.n_vac; s += 256) GV[s] = a.vgeom[s];
     }
     // pixel pools: a workgroup whose pass was drained before it started ends at once (a launch
     // has many more workgroups than fit, and the late ones of a pass find it drained): threads
@@ -1411,8 +1425,14 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                     // result is the same in any order.
                     if constexpr (!kBVH) {
                         const int c = total - base;                        // uniform
+                        // a round of VLP rays only: the non-emitters' list (IntersectPVacuumDevice
+                        // never counts an emitter), which often fits fewer lane-group iterations
+                        // (cornell: 8 spheres instead of 9)
+                        const bool allvac = BDPT_VAC_LIST && !kPool && base >= cn;   // uniform
+                        const int nl = allvac ? a.n_vac : n;
+                        const float4* GL = allvac ? GV : G;
                         int lg = c <= 8 ? 3 : (c <= 16 ? 2 : (c <= 32 ? 1 : 0));
-                        while (lg > 0 && (1 << lg) > n) lg--;
+                        while (lg > 0 && (1 << lg) > nl) lg--;
                         if (lg > 0) {
                             BDPT_CNTN(8, 1);
                             const int rpg = 64 >> lg;
@@ -1425,6 +1445,17 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
 #if BDPT_IKEY
                                 const unsigned km = maxt_key(r0.w);
 #endif
+                                if (allvac) {
+                                    for (int s = nl - 1 - g; s >= 0; s -= 1 << lg) {
+                                        const troots q = sphere_roots(GL[s], o, d);
+#if BDPT_IKEY
+                                        if (umin2(key_of(q.t1), key_of(q.t2)) < km) { occ = 1; break; }
+#else
+                                        const float rr = q.t1 > kEps ? q.t1 : q.t2;
+                                        if (q.t2 > kEps && rr < r0.w) { occ = 1; break; }
+#endif
+                                    }
+                                } else
                                 for (int s = n - 1 - g; s >= 0; s -= 1 << lg) {
                                     BDPT_CNTN(16, 1);
                                     const troots q = sphere_roots(G[s], o, d);

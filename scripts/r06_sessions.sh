@@ -239,4 +239,25 @@ s22() {
   done
 }
 
+s23() {
+  # VLP-only part-full shadow rounds over the non-emitters' list (BDPT_VAC_LIST) on top of the
+  # emitter skip in full rounds (BDPT_VAC_SKIP): parity first, then A/B
+  pytest_gpu s23_pytest_parity.log tests/test_gpu_parity.py tests/test_gpu_fuzz.py tests/test_gpu_configs.py -k "not config4" || exit 1
+  for w in cornell1080 weak64 caustic8; do
+    MODE=bench ARGS="--workload $w --no-cpu-baseline" ROUNDS=2 \
+      VARIANTS="list: skiponly:BDPT_JIT_FLAGS=-DBDPT_VAC_LIST=0 none:BDPT_JIT_FLAGS=-DBDPT_VAC_LIST=0,-DBDPT_VAC_SKIP=0" \
+      OUT=gpurun_out/s23_ab_vac_list.txt bash scripts/ab.sh || exit 1
+  done
+}
+
+s24() {
+  # the list kept out of the pool build and the precompiled instances: full GPU suite, then A/B
+  pytest_gpu s24_pytest_gpu.log tests || exit 1
+  for w in cornell1080 caustic8 weak64; do
+    MODE=bench ARGS="--workload $w --no-cpu-baseline" ROUNDS=2 \
+      VARIANTS="list: skiponly:BDPT_JIT_FLAGS=-DBDPT_VAC_LIST=0" \
+      OUT=gpurun_out/s24_ab_vac_list.txt bash scripts/ab.sh || exit 1
+  done
+}
+
 "$@"

@@ -41,8 +41,12 @@ def jit_defines(spheres):
         parts.append("{" + ",".join(hexf(x) for x in (s["p"][0], s["p"][1], s["p"][2], rr)) + "}")
         if any(float(e) != 0.0 for e in s["e"]):
             emis |= 1 << i
-    return [f"-DBDPT_JIT_N={len(spheres)}", f"-DBDPT_JIT_EMIS={emis}ull", "-DBDPT_JIT_GEOM={" + ",".join(parts) + "}",
-            f"-DBDPT_JIT_ZERO_SAFE={int(zero_exit_safe(spheres))}"]
+    n = len(spheres)
+    n_vac = n - bin(emis).count("1")
+    # bdpt_host.cpp jit_path_kernel: the non-emitters' list only where it saves a lane-group iteration
+    vac_list = any((1 << k) <= n_vac and -(-n_vac >> k) < -(-n >> k) for k in (1, 2, 3))
+    return [f"-DBDPT_JIT_N={n}", f"-DBDPT_JIT_EMIS={emis}ull", "-DBDPT_JIT_GEOM={" + ",".join(parts) + "}",
+            f"-DBDPT_JIT_ZERO_SAFE={int(zero_exit_safe(spheres))}"] + ([] if vac_list else ["-DBDPT_VAC_LIST=0"])
 
 
 def zero_exit_safe(spheres):
