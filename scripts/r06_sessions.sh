@@ -260,4 +260,35 @@ s24() {
   done
 }
 
+s25() {
+  # per-section shares of the cornell1080 kernel after the VLP-round changes
+  RUNS="cornell1080:64" bash scripts/section_profile.sh || exit 1
+}
+
+s26() {
+  # final-build rocprof stats + PMC records, cornell1080 in each mode the auto choice can take
+  WORKLOADS="cornell1080:64:cornell1080:BDPT_UNITS=8 cornell1080:64:cornell1080s64:BDPT_UNITS=0 cornell1080:32:cornell1080s32:BDPT_UNITS=0" \
+    bash scripts/profile_workloads.sh
+}
+
+s27() {
+  # final-build rocprof stats + PMC records: caustic8 (pools), weak64 at both stream counts
+  WORKLOADS="caustic8:128:caustic8:BDPT_POOL=16 weak64:32 weak64:16:weak64s16:BDPT_UNITS=0" \
+    bash scripts/profile_workloads.sh
+}
+
+s28() {
+  # the final tree as the driver runs it: GPU suite, smoke, default bench; then the other
+  # workloads' bench lines with the CPU leg
+  pytest_gpu s28_pytest_gpu.log tests || exit 1
+  timeout -k 10 300 python -c "import __graft_entry__ as e; e.smoke()" > gpurun_out/s28_smoke.log 2>&1 || { tail -20 gpurun_out/s28_smoke.log; exit 1; }
+  tail -1 gpurun_out/s28_smoke.log
+  for w in default caustic8 weak64; do
+    a=""; [ $w != default ] && a="--workload $w"
+    timeout -k 10 400 python bench.py $a > gpurun_out/s28_bench_$w.log 2>&1 || { tail -20 gpurun_out/s28_bench_$w.log; exit 1; }
+    grep '^{' gpurun_out/s28_bench_$w.log | tail -1 > gpurun_out/s28_bench_$w.json
+    python3 -c "import json; d=json.load(open('gpurun_out/s28_bench_$w.json')); r=d['roofline']; print('$w', d['value'], d['ms_per_step'], r['frac'], r['avg_launch_ms'], r.get('traffic_over_model'), r.get('valu_busy_pmc'), d.get('speedup_vs_cpu_node_estimate'))"
+  done
+}
+
 "$@"
