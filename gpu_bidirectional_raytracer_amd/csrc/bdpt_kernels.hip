@@ -255,6 +255,13 @@ __device__ __forceinline__ f3 cosine_tail(f3 w, f3 u, float u_phi, float u_r2, f
 #ifndef BDPT_VAC_SKIP
 #define BDPT_VAC_SKIP 1
 #endif
+// Lane groups of a part-full shadow round: 2^lg groups for rounds of <= 64 / 2^lg rays (lg <= 5),
+// reduced only while fewer groups take as few iterations -- caustic's 3 spheres in 1 iteration
+// instead of 2, cornell's 9 in 1 for rounds of <= 4 rays (BDPT_LG_RULE=0: the round-5 rule, lg <= 3,
+// reduced while 2^lg exceeds the list)
+#ifndef BDPT_LG_RULE
+#define BDPT_LG_RULE 1
+#endif
 // The same rounds when they are part-full (<= 32 rays, traced by lane groups that split the sphere
 // list): the groups split the non-emitters' list (bdpt_path_args.vgeom, staged in LDS as GV).
 // Not in the pixel-pool build: caustic8 ran 2 % slower with it (profiles/r06_s23_ab_vac_list.txt);
@@ -1431,8 +1438,16 @@ void bdpt_path_kernel_t(bdpt_path_args a) {
                         const bool allvac = BDPT_VAC_LIST && !kPool && base >= cn;   // uniform
                         const int nl = allvac ? a.n_vac : n;
                         const float4* GL = allvac ? GV : G;
+#if BDPT_LG_RULE
+                        // as many groups as the round's rays allow, down to the fewest that still
+                        // take the same number of iterations (ceil(nl / 2^lg)); groups past the
+                        // list's end idle
+                        int lg = c <= 2 ? 5 : c <= 4 ? 4 : c <= 8 ? 3 : (c <= 16 ? 2 : (c <= 32 ? 1 : 0));
+                        while (lg > 0 && (1 << (lg - 1)) >= nl) lg--;
+#else
                         int lg = c <= 8 ? 3 : (c <= 16 ? 2 : (c <= 32 ? 1 : 0));
                         while (lg > 0 && (1 << lg) > nl) lg--;
+#endif
                         if (lg > 0) {
                             BDPT_CNTN(8, 1);
                             const int rpg = 64 >> lg;

@@ -291,4 +291,14 @@ s28() {
   done
 }
 
+s29() {
+  # the lane-group rule of part-full shadow rounds (BDPT_LG_RULE): parity first, then A/B
+  pytest_gpu s29_pytest_parity.log tests/test_gpu_parity.py tests/test_gpu_fuzz.py tests/test_gpu_pool.py || exit 1
+  for w in cornell1080 caustic8 weak64; do
+    MODE=bench ARGS="--workload $w --no-cpu-baseline" ROUNDS=2 \
+      VARIANTS="rule: old:BDPT_JIT_FLAGS=-DBDPT_LG_RULE=0" \
+      OUT=gpurun_out/s29_ab_lg_rule.txt bash scripts/ab.sh || exit 1
+  done
+}
+
 "$@"

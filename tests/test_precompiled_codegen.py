@@ -11,8 +11,8 @@ Recorded values and why they are acceptable:
   * the per-N instances hold the scene geometry in SGPRs (wave-uniform constant loads); from
     N = 12 spheres (fused) / 13 (pass streams) the SGPR file (106) overflows and the excess goes to
     VGPR lanes (v_writelane / v_readlane, no memory traffic): fused 2 per sphere above 11, pass
-    streams 3, 5, 7, 9 for N = 13..16 (from N = 11, 2 per sphere above 10, before the VLP-only
-    shadow rounds skipped the emitters, BDPT_VAC_SKIP).  These instances only run with
+    streams 2, 3, 6, 7, 9 for N = 12..16 (from N = 11, 2 per sphere above 10, before the VLP-only
+    shadow rounds skipped the emitters, BDPT_VAC_SKIP, and the lane-group rule BDPT_LG_RULE).  These instances only run with
     specialisation off: by default a <= 64-sphere scene runs its hipRTC build;
   * the BVH instance keeps its traversal state in SGPRs and moves 10 (pass streams) / 2 (fused)
     of them to VGPR lanes in the same way (11 / 3 before round 4's settled pass-stream randoms
@@ -37,7 +37,7 @@ def _sgpr_spills(n, streams):
     if n == -1:
         return 11 if streams else 2   # (streams: 10 before the d_scp descriptor, BDPT_SCP)
     if streams:
-        return 2 * (n - 12) + 1 if n > 12 else 0
+        return {12: 2, 13: 3, 14: 6, 15: 7, 16: 9}.get(n, 0)
     return 2 * (n - 11) if n > 11 else 0
 
 
