@@ -301,4 +301,34 @@ s29() {
   done
 }
 
+s31() {
+  # the VLP-round changes on the two-light and mirror scenes (sweep spread check), one session
+  for sc in cornell_2luci synthetic64 hall_of_mirrors; do
+    MODE=bench ARGS="--scene $sc --no-cpu-baseline --passes 32 --steps 10" ROUNDS=2 \
+      VARIANTS="final: off:BDPT_JIT_FLAGS=-DBDPT_VAC_LIST=0,-DBDPT_VAC_SKIP=0,-DBDPT_LG_RULE=0" \
+      OUT=gpurun_out/s31_ab_scenes.txt bash scripts/ab.sh || exit 1
+  done
+}
+
+s32() {
+  # cornell_2luci (two emitters): which of the three shadow-round changes costs, fixed 16 streams
+  for sc in cornell_2luci hall_of_mirrors; do
+    MODE=bench ARGS="--scene $sc --no-cpu-baseline --passes 32 --steps 10 --streams 16" ROUNDS=2 \
+      VARIANTS="final: noskip:BDPT_JIT_FLAGS=-DBDPT_VAC_SKIP=0 nolist:BDPT_JIT_FLAGS=-DBDPT_VAC_LIST=0 oldlg:BDPT_JIT_FLAGS=-DBDPT_LG_RULE=0 off:BDPT_JIT_FLAGS=-DBDPT_VAC_LIST=0,-DBDPT_VAC_SKIP=0,-DBDPT_LG_RULE=0" \
+      OUT=gpurun_out/s32_ab_flags.txt bash scripts/ab.sh || exit 1
+  done
+}
+
+s33() {
+  # the non-emitters' list made opt-in (BDPT_VAC_LIST=1): parity, cornell1080 / cornell_2luci A/B,
+  # then cornell1080's profiles on the default build
+  pytest_gpu s33_pytest_parity.log tests/test_gpu_parity.py tests/test_gpu_fuzz.py tests/test_gpu_configs.py -k "not config4" || exit 1
+  MODE=bench ARGS="--workload cornell1080 --no-cpu-baseline" ROUNDS=2 \
+    VARIANTS="default: list:BDPT_VAC_LIST=1" OUT=gpurun_out/s33_ab_list_optin.txt bash scripts/ab.sh || exit 1
+  MODE=bench ARGS="--scene cornell_2luci --no-cpu-baseline --passes 32 --steps 10 --streams 16" ROUNDS=2 \
+    VARIANTS="default: list:BDPT_VAC_LIST=1" OUT=gpurun_out/s33_ab_list_optin.txt bash scripts/ab.sh || exit 1
+  WORKLOADS="cornell1080:64:cornell1080:BDPT_UNITS=8 cornell1080:64:cornell1080s64:BDPT_UNITS=0 cornell1080:32:cornell1080s32:BDPT_UNITS=0" \
+    bash scripts/profile_workloads.sh
+}
+
 "$@"
