@@ -331,4 +331,13 @@ s33() {
     bash scripts/profile_workloads.sh
 }
 
+s34() {
+  # the tree rebuilt in a fresh container (same sources as s28): GPU suite, smoke, default bench
+  pytest_gpu s34_pytest_gpu.log tests || exit 1
+  timeout -k 10 300 python -c "import __graft_entry__ as e; e.smoke()" > gpurun_out/s34_smoke.log 2>&1 || { tail -20 gpurun_out/s34_smoke.log; exit 1; }
+  tail -1 gpurun_out/s34_smoke.log
+  timeout -k 10 400 python bench.py > gpurun_out/s34_bench_default.log 2>&1 || { tail -20 gpurun_out/s34_bench_default.log; exit 1; }
+  grep '^{' gpurun_out/s34_bench_default.log | tail -1
+}
+
 "$@"
